@@ -1,0 +1,208 @@
+// fwav_affine.hip — batched affine least squares with mirror + first-minimum select (bit-exact).
+//
+// Replaces (reference /root/reference/fractal.py):
+//   _flush_gpu_batch   :852-870
+//   _process_gpu_batch :757-850   for range b and slot j over [K candidates | K mirrored]:
+//       r̄ = mean(R); r̃ = R − r̄; d̄ = mean(D); d̃ = D − d̄; s = Σd̃r̃ / (Σd̃d̃ + 1e-12); o = r̄ − s·d̄;
+//       err = ‖(s·D + o) − R‖₂; err = +inf where cand < 0; j* = argmin(err) (first); emit
+//       (cand_clamped[j*], clip(s, ±s_clip), o, j* ≥ K, err)            (quirks Q3, Q4)
+//   The reference's corr/min_err (:807-808) are dead and not computed.
+//
+// One wave per range, lane c ↔ candidate c (c, c+64, …): the lane gathers its pool row once and
+// evaluates both orientations from registers (mirror = reversed register index).  Reductions are numpy
+// pairwise order over rs, every op a separately rounded f32 op (-ffp-contract=off): bit-exact with the
+// reference (tests/test_gpu_parity.py).  The argmin is a 6-step xor-shuffle reduction with numpy's
+// tie/NaN rules (first NaN wins, else smallest err, else lowest slot).
+// Bytes per range: 4·rs (range) + 4·K (candidates) + 4·K·rs (gathered rows) + 17 (outputs).
+#include "fwav_common.h"
+
+namespace fwav {
+
+constexpr int kAffWaves = 4;
+
+struct Best {
+  float err, s, o;
+  int slot, dom;
+};
+
+__device__ __forceinline__ bool better(float e1, int s1, float e2, int s2) {
+  const bool n1 = e1 != e1, n2 = e2 != e2;
+  if (n1 || n2) return (n1 && n2) ? s1 < s2 : n1;
+  return e1 < e2 || (e1 == e2 && s1 < s2);
+}
+
+template <int RS>
+__device__ __forceinline__ void eval_orient(const float (&X)[RS], const float (&R)[RS], const float (&rc)[RS], float rm,
+                                            float& s, float& o, float& err) {
+  auto fx = [&](int i) { return X[i]; };
+  const float dm = pw_sum_n<RS>(fx) / (float)RS;
+  float dc[RS];
+#pragma unroll
+  for (int i = 0; i < RS; ++i) dc[i] = X[i] - dm;
+  auto fn = [&](int i) { return dc[i] * rc[i]; };
+  auto fd = [&](int i) { return dc[i] * dc[i]; };
+  const float num = pw_sum_n<RS>(fn);
+  const float den = pw_sum_n<RS>(fd) + 1e-12f;
+  s = num / den;
+  o = rm - s * dm;
+  auto fe = [&](int i) {
+    const float df = (s * X[i] + o) - R[i];
+    return df * df;
+  };
+  err = sqrtf(pw_sum_n<RS>(fe));
+}
+
+template <int RS>
+__global__ __launch_bounds__(64 * kAffWaves) void k_affine(const float* __restrict__ ranges, int64_t nr,
+                                                           const int32_t* __restrict__ cand, int K,
+                                                           const float* __restrict__ pool, float s_clip,
+                                                           int32_t* __restrict__ out_idx, float* __restrict__ out_s,
+                                                           float* __restrict__ out_o, uint8_t* __restrict__ out_sym,
+                                                           float* __restrict__ out_err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * kAffWaves + (threadIdx.x >> 6);
+  if (r >= nr) return;
+  float R[RS], rc[RS];
+#pragma unroll
+  for (int i = 0; i < RS; ++i) R[i] = ranges[r * RS + i];
+  auto fr = [&](int i) { return R[i]; };
+  const float rm = pw_sum_n<RS>(fr) / (float)RS;
+#pragma unroll
+  for (int i = 0; i < RS; ++i) rc[i] = R[i] - rm;
+
+  Best b{INFINITY, 0.f, 0.f, 0x7fffffff, 0};
+  bool have = false;
+  const int32_t* cr = cand + r * (int64_t)K;
+  for (int c = lane; c < K; c += 64) {
+    const int32_t ci = cr[c];
+    const int32_t di = ci < 0 ? 0 : ci;
+    float D[RS], M[RS];
+    if constexpr (RS % 4 == 0) {
+      const float4* p = reinterpret_cast<const float4*>(pool + (int64_t)di * RS);
+#pragma unroll
+      for (int j = 0; j < RS / 4; ++j) {
+        float4 v = p[j];
+        D[4 * j] = v.x; D[4 * j + 1] = v.y; D[4 * j + 2] = v.z; D[4 * j + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < RS; ++i) D[i] = pool[(int64_t)di * RS + i];
+    }
+#pragma unroll
+    for (int i = 0; i < RS; ++i) M[i] = D[RS - 1 - i];
+    float s0, o0, e0, s1, o1, e1;
+    eval_orient<RS>(D, R, rc, rm, s0, o0, e0);
+    eval_orient<RS>(M, R, rc, rm, s1, o1, e1);
+    if (ci < 0) { e0 = INFINITY; e1 = INFINITY; }
+    if (!have || better(e0, c, b.err, b.slot)) { b = Best{e0, s0, o0, c, di}; have = true; }
+    if (better(e1, K + c, b.err, b.slot)) b = Best{e1, s1, o1, K + c, di};
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    Best o;
+    o.err = __shfl_xor(b.err, m);
+    o.s = __shfl_xor(b.s, m);
+    o.o = __shfl_xor(b.o, m);
+    o.slot = __shfl_xor(b.slot, m);
+    o.dom = __shfl_xor(b.dom, m);
+    if (better(o.err, o.slot, b.err, b.slot)) b = o;
+  }
+  if (lane == 0) {
+    out_idx[r] = b.dom;
+    out_s[r] = clip_sym(b.s, fabsf(s_clip));
+    out_o[r] = b.o;
+    out_sym[r] = (uint8_t)(b.slot >= K);
+    out_err[r] = b.err;
+  }
+}
+
+// Generic rs (runtime), rows read from global memory; same arithmetic.
+__global__ __launch_bounds__(64 * kAffWaves) void k_affine_any(const float* __restrict__ ranges, int64_t nr, int rs,
+                                                               const int32_t* __restrict__ cand, int K,
+                                                               const float* __restrict__ pool, float s_clip,
+                                                               int32_t* __restrict__ out_idx, float* __restrict__ out_s,
+                                                               float* __restrict__ out_o, uint8_t* __restrict__ out_sym,
+                                                               float* __restrict__ out_err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * kAffWaves + (threadIdx.x >> 6);
+  if (r >= nr) return;
+  const float* R = ranges + r * rs;
+  auto fr = [&](int i) { return R[i]; };
+  const float rm = pw_sum(fr, rs) / (float)rs;
+  Best b{INFINITY, 0.f, 0.f, 0x7fffffff, 0};
+  bool have = false;
+  const int32_t* cr = cand + r * (int64_t)K;
+  for (int c = lane; c < K; c += 64) {
+    const int32_t ci = cr[c];
+    const int32_t di = ci < 0 ? 0 : ci;
+    const float* D = pool + (int64_t)di * rs;
+    for (int orient = 0; orient < 2; ++orient) {
+      auto X = [&](int i) { return orient ? D[rs - 1 - i] : D[i]; };
+      const float dm = pw_sum(X, rs) / (float)rs;
+      auto fn = [&](int i) { return (X(i) - dm) * (R[i] - rm); };
+      auto fd = [&](int i) {
+        const float t = X(i) - dm;
+        return t * t;
+      };
+      const float num = pw_sum(fn, rs);
+      const float den = pw_sum(fd, rs) + 1e-12f;
+      const float s = num / den;
+      const float o = rm - s * dm;
+      auto fe = [&](int i) {
+        const float df = (s * X(i) + o) - R[i];
+        return df * df;
+      };
+      float e = sqrtf(pw_sum(fe, rs));
+      if (ci < 0) e = INFINITY;
+      const int slot = orient * K + c;
+      if (!have || better(e, slot, b.err, b.slot)) { b = Best{e, s, o, slot, di}; have = true; }
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    Best o;
+    o.err = __shfl_xor(b.err, m);
+    o.s = __shfl_xor(b.s, m);
+    o.o = __shfl_xor(b.o, m);
+    o.slot = __shfl_xor(b.slot, m);
+    o.dom = __shfl_xor(b.dom, m);
+    if (better(o.err, o.slot, b.err, b.slot)) b = o;
+  }
+  if (lane == 0) {
+    out_idx[r] = b.dom;
+    out_s[r] = clip_sym(b.s, fabsf(s_clip));
+    out_o[r] = b.o;
+    out_sym[r] = (uint8_t)(b.slot >= K);
+    out_err[r] = b.err;
+  }
+}
+
+}  // namespace fwav
+
+using namespace fwav;
+
+extern "C" {
+
+int fwav_affine(const float* ranges, int64_t nr, int rs, const int32_t* cand, int K, const float* pool, int64_t nd,
+                float s_clip, int32_t* out_idx, float* out_s, float* out_o, uint8_t* out_sym, float* out_err,
+                void* stream) {
+  FWAV_CHECK_ARG(ranges && cand && pool && out_idx && out_s && out_o && out_sym && out_err, FWAV_ERR_ARG,
+                 "fwav_affine: null pointer");
+  FWAV_CHECK_ARG(nr >= 0 && rs >= 1 && K >= 1 && nd >= 1, FWAV_ERR_SHAPE, "fwav_affine: bad shape");
+  FWAV_CHECK_ARG(rs <= kMaxPairwise, FWAV_ERR_SHAPE, "fwav_affine: rs > %d", kMaxPairwise);
+  if (nr == 0) return FWAV_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t grid = cdiv(nr, kAffWaves);
+  const int thr = 64 * kAffWaves;
+  switch (rs) {
+    case 4: k_affine<4><<<grid, thr, 0, st>>>(ranges, nr, cand, K, pool, s_clip, out_idx, out_s, out_o, out_sym, out_err); break;
+    case 8: k_affine<8><<<grid, thr, 0, st>>>(ranges, nr, cand, K, pool, s_clip, out_idx, out_s, out_o, out_sym, out_err); break;
+    case 16: k_affine<16><<<grid, thr, 0, st>>>(ranges, nr, cand, K, pool, s_clip, out_idx, out_s, out_o, out_sym, out_err); break;
+    default:
+      k_affine_any<<<grid, thr, 0, st>>>(ranges, nr, rs, cand, K, pool, s_clip, out_idx, out_s, out_o, out_sym, out_err);
+  }
+  FWAV_LAUNCH_CHECK("fwav_affine");
+  return FWAV_OK;
+}
+
+}  // extern "C"

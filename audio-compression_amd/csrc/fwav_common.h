@@ -1,0 +1,118 @@
+// fwav_common.h — shared device helpers for the MI355X (gfx950) fractal-WAV kernels.
+//
+// Arithmetic contract (pinned by oracle/fractal_oracle.py against the reference
+// goldens): every reduction is numpy's pairwise_sum order with numpy's initial "0 +", every elementwise op is
+// one separately rounded f32 op.  The library is compiled with -ffp-contract=off and correctly rounded f32
+// divide/sqrt, so `a * b + c` below is two roundings, exactly as numpy evaluates it.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+namespace fwav {
+
+// ----------------------------------------------------------------------------------------- status
+// Thread-local last-error string returned by fwav_last_error(); no exceptions cross the C ABI.
+void set_error(const char* fmt, ...);
+
+#define FWAV_CHECK_ARG(cond, code, ...)        \
+  do {                                         \
+    if (!(cond)) {                             \
+      ::fwav::set_error(__VA_ARGS__);          \
+      return (code);                           \
+    }                                          \
+  } while (0)
+
+#define FWAV_LAUNCH_CHECK(what)                                                         \
+  do {                                                                                  \
+    hipError_t e_ = hipGetLastError();                                                  \
+    if (e_ != hipSuccess) {                                                             \
+      ::fwav::set_error("%s: %s", (what), hipGetErrorString(e_));                       \
+      return FWAV_ERR_HIP;                                                              \
+    }                                                                                   \
+  } while (0)
+
+constexpr int kWave = 64;
+
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ----------------------------------------------------------------------- numpy pairwise reductions
+// pairwise_sum (numpy loops_utils.h.src) of f(off .. off+n-1):
+//   n < 8: sequential from 0;  8 <= n <= 128: 8 strided accumulators + tree + sequential tail;
+//   n > 128: split at n2 = n/2 - (n/2)%8 and add the halves.
+template <class F>
+__device__ __forceinline__ float pw_leaf(const F& f, int off, int n) {
+  if (n < 8) {
+    float r = 0.0f;
+    for (int i = 0; i < n; ++i) r = r + f(off + i);
+    return r;
+  }
+  float r0 = f(off + 0), r1 = f(off + 1), r2 = f(off + 2), r3 = f(off + 3);
+  float r4 = f(off + 4), r5 = f(off + 5), r6 = f(off + 6), r7 = f(off + 7);
+  const int m = n - (n & 7);
+  for (int i = 8; i < m; i += 8) {
+    r0 = r0 + f(off + i + 0);
+    r1 = r1 + f(off + i + 1);
+    r2 = r2 + f(off + i + 2);
+    r3 = r3 + f(off + i + 3);
+    r4 = r4 + f(off + i + 4);
+    r5 = r5 + f(off + i + 5);
+    r6 = r6 + f(off + i + 6);
+    r7 = r7 + f(off + i + 7);
+  }
+  float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (int i = m; i < n; ++i) res = res + f(off + i);
+  return res;
+}
+
+template <int D, class F>
+__device__ __forceinline__ float pw_rec(const F& f, int off, int n) {
+  if constexpr (D == 0) {
+    return pw_leaf(f, off, n);
+  } else {
+    if (n <= 128) return pw_leaf(f, off, n);
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return pw_rec<D - 1>(f, off, n2) + pw_rec<D - 1>(f, off + n2, n - n2);
+  }
+}
+
+// np.add.reduce over n <= kMaxPairwise elements: numpy starts the output at 0 (so -0 sums to +0).
+constexpr int kMaxPairwise = 1024;
+template <class F>
+__device__ __forceinline__ float pw_sum(const F& f, int n) {
+  return 0.0f + pw_rec<3>(f, 0, n);
+}
+
+// Compile-time-length variant (fully unrolled, register-resident operands).
+template <int N, class F>
+__device__ __forceinline__ float pw_sum_n(const F& f) {
+  return 0.0f + pw_rec<3>(f, 0, N);
+}
+
+// np.clip(x, -c, c) keeps NaN (comparisons false).
+__device__ __forceinline__ float clip_sym(float x, float c) { return x < -c ? -c : (x > c ? c : x); }
+
+// Order-preserving map of f32 to u32 (larger float → larger key; NaN above +inf).
+__device__ __forceinline__ uint32_t f2key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+}  // namespace fwav
+
+// C-ABI status codes (mirrored in include/fwav.h).
+#define FWAV_OK 0
+#define FWAV_ERR_ARG (-1)
+#define FWAV_ERR_SHAPE (-2)
+#define FWAV_ERR_K (-3)
+#define FWAV_ERR_HIP (-4)
+#define FWAV_ERR_WORKSPACE (-5)

@@ -1,0 +1,275 @@
+// fwav_signal.hip — voiced detection, range formation and the energy prune, on device.
+//
+// Replaces (reference /root/reference/fractal.py):
+//   voiced_detection            :880-909   frame energy → 5-tap smoothing → hysteresis → per-sample mask
+//   compress_audio range setup  :1079-1112 signal·mask, reflect pad to a multiple of rs, reshape
+//   cpu_worker energy prune     :601-603   mean(r²) < 0.75·thr  → no candidates (all −1)
+//
+// The hysteresis loop (:902-907) is sequential in the reference; here a frame's state is the decision of
+// the last frame that was > hi (voiced) or < lo (unvoiced), found with a max-scan over positions:
+//   k_voiced_decide (per frame, + per-block last decisive position) → k_voiced_carry (one block, exclusive
+//   prefix max over blocks) → k_frame_state (in-block max-scan + carry) → k_form_ranges (per sample).
+#include "fwav_common.h"
+
+namespace fwav {
+
+__device__ __forceinline__ int64_t reflect_idx(int64_t p, int64_t n) {
+  // np.pad(mode='reflect') index for p >= 0 on the right side (period 2(n-1)).
+  if (p < n) return p;
+  if (n == 1) return 0;
+  const int64_t period = 2 * (n - 1);
+  int64_t q = p % period;
+  return q < n ? q : period - q;
+}
+
+constexpr int kFramesPerBlock = 1024;
+constexpr int kSignalThreads = 256;
+
+// smoothed energy of frame i; mirrors numpy correlate 'same' with a symmetric kernel (oracle smooth5).
+__device__ __forceinline__ float smooth_at(const float* e, int64_t nf, int64_t i, int w, float k) {
+  const int left = w / 2;
+  int64_t lo = i - left, hi = i - left + w;  // window [lo, hi)
+  if (lo < 0) lo = 0;
+  if (hi > nf) hi = nf;
+  float s = 0.0f;
+  for (int64_t j = lo; j < hi; ++j) s = s + e[j] * k;
+  return s;
+}
+
+__global__ void k_frame_energy(const float* __restrict__ sig, int64_t n, int frame, int64_t nf,
+                               float* __restrict__ energy) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nf) return;
+  const int64_t base = i * frame;
+  auto sq = [&](int j) {
+    float x = sig[reflect_idx(base + j, n)];
+    return x * x;
+  };
+  energy[i] = pw_sum(sq, frame) / (float)frame;
+}
+
+// dec[i] ∈ {1 voiced, 0 unvoiced, -1 keep};  blast[b] = last decisive frame position in block b or -1.
+__global__ void k_voiced_decide(const float* __restrict__ energy, int64_t nf, int w, float k, float hi,
+                                float lo, int8_t* __restrict__ dec, int64_t* __restrict__ blast) {
+  __shared__ int64_t red[kSignalThreads / kWave];
+  const int64_t b0 = (int64_t)blockIdx.x * kFramesPerBlock;
+  int64_t last = -1;
+  for (int t = threadIdx.x; t < kFramesPerBlock; t += blockDim.x) {
+    int64_t i = b0 + t;
+    if (i >= nf) break;
+    float es = smooth_at(energy, nf, i, w, k);
+    int8_t d = es > hi ? 1 : (es < lo ? 0 : -1);
+    dec[i] = d;
+    if (d >= 0) last = i > last ? i : last;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t v = __shfl_xor(last, o);
+    last = v > last ? v : last;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t m = -1;
+    for (int j = 0; j < (int)(blockDim.x / kWave); ++j) m = red[j] > m ? red[j] : m;
+    blast[blockIdx.x] = m;
+  }
+}
+
+// carry[b] = max(blast[0..b-1]) (exclusive), one block.
+__global__ void k_voiced_carry(const int64_t* __restrict__ blast, int64_t nb, int64_t* __restrict__ carry) {
+  __shared__ int64_t wsum[1024 / kWave];
+  __shared__ int64_t running;
+  if (threadIdx.x == 0) running = -1;
+  __syncthreads();
+  for (int64_t c = 0; c < nb; c += blockDim.x) {
+    int64_t i = c + threadIdx.x;
+    int64_t v = i < nb ? blast[i] : -1;
+    // inclusive max-scan within the wave
+    const int lane = threadIdx.x & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+      int64_t u = __shfl_up(v, o);
+      if (lane >= o) v = u > v ? u : v;
+    }
+    if (lane == 63) wsum[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int64_t pre = running;
+    for (int j = 0; j < (int)(threadIdx.x >> 6); ++j) pre = wsum[j] > pre ? wsum[j] : pre;
+    int64_t incl = v > pre ? v : pre;
+    int64_t excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = pre;
+    if (i < nb) carry[i] = excl;
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) running = incl;
+    __syncthreads();
+  }
+}
+
+// state[f] = decision of the last decisive frame <= f (0 if none): block max-scan of positions + carry.
+__global__ void k_frame_state(const int8_t* __restrict__ dec, const int64_t* __restrict__ carry, int64_t nf,
+                              uint8_t* __restrict__ state) {
+  __shared__ int64_t wlast[kSignalThreads / kWave];
+  constexpr int kPer = kFramesPerBlock / kSignalThreads;  // 4 consecutive frames per thread
+  const int64_t f0 = (int64_t)blockIdx.x * kFramesPerBlock + (int64_t)threadIdx.x * kPer;
+  int64_t pos[kPer];
+  int64_t run = -1;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    int64_t f = f0 + j;
+    if (f < nf && dec[f] >= 0) run = f;
+    pos[j] = run;
+  }
+  // exclusive max-scan of the per-thread last position across the block
+  const int lane = threadIdx.x & 63;
+  int64_t v = run;
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t u = __shfl_up(v, o);
+    if (lane >= o) v = u > v ? u : v;
+  }
+  if (lane == 63) wlast[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int64_t pre = carry[blockIdx.x];
+  for (int j = 0; j < (int)(threadIdx.x >> 6); ++j) pre = wlast[j] > pre ? wlast[j] : pre;
+  int64_t ex = __shfl_up(v, 1);
+  if (lane == 0) ex = -1;
+  pre = ex > pre ? ex : pre;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    int64_t f = f0 + j;
+    if (f >= nf) break;
+    int64_t p = pos[j] >= 0 ? pos[j] : pre;
+    state[f] = p >= 0 ? (uint8_t)dec[p] : (uint8_t)0;
+  }
+}
+
+// ranges[p] = (signal · mask)[reflect(p)] for p < nr·rs (fractal.py:1079, 1095-1097).
+__global__ void k_form_ranges(const float* __restrict__ sig, int64_t n, int frame, const uint8_t* __restrict__ state,
+                              int64_t total, float* __restrict__ ranges, uint8_t* __restrict__ mask_out) {
+  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= total) return;
+  int64_t src = reflect_idx(p, n);
+  uint8_t m = state[src / frame];
+  ranges[p] = sig[src] * (float)m;
+  if (mask_out != nullptr && p < n) mask_out[p] = m;
+}
+
+// Σ (signal·mask)² in f64, one partial per block (the silent-input test, fractal.py:1083).
+__global__ void k_weighted_energy(const float* __restrict__ ranges, int64_t n, double* __restrict__ partial) {
+  __shared__ double red[kSignalThreads / kWave];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double x = ranges[i];
+    acc += x * x;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int j = 0; j < (int)(blockDim.x / kWave); ++j) s += red[j];
+    partial[blockIdx.x] = s;
+  }
+}
+
+// Energy prune + degenerate queries + active list (fractal.py:598-622, quirk Q1/Q3/Q11).
+//   pruned            → cand row all −1
+//   query row all 0   → cand row 0..min(K,nd)−1 (every score is 0: the (score desc, index asc) order)
+//   otherwise         → appended to `active` for the similarity search
+__global__ void k_prune(const float* __restrict__ ranges, int64_t nr, int64_t q_offset, int rs, float thr,
+                        int fast_mode, const float* __restrict__ emb, int64_t nd, int k, int32_t* __restrict__ cand,
+                        int32_t* __restrict__ active, int32_t* __restrict__ n_active) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nr) return;
+  const float* r = ranges + i * rs;
+  auto sq = [&](int j) { return r[j] * r[j]; };
+  bool pruned = fast_mode && (pw_sum(sq, rs) / (float)rs < thr);
+  bool zero = true;
+  if (!pruned) {
+    const float4* q = reinterpret_cast<const float4*>(emb + (i + q_offset) * 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float4 v = q[j];
+      zero = zero && v.x == 0.0f && v.y == 0.0f && v.z == 0.0f && v.w == 0.0f;
+    }
+  }
+  int32_t* c = cand + i * (int64_t)k;
+  if (pruned) {
+    for (int j = 0; j < k; ++j) c[j] = -1;
+  } else if (zero) {
+    for (int j = 0; j < k; ++j) c[j] = j < nd ? j : -1;
+  } else {
+    int slot = atomicAdd(n_active, 1);
+    active[slot] = (int32_t)i;
+  }
+}
+
+}  // namespace fwav
+
+using namespace fwav;
+
+extern "C" {
+
+size_t fwav_voiced_workspace_size(int64_t n, int frame) {
+  const int64_t nf = cdiv(n, frame);
+  const int64_t nb = cdiv(nf, kFramesPerBlock);
+  return (size_t)(2 * nb * sizeof(int64_t) + nf * sizeof(float) + 2 * nf + 64);
+}
+
+// Voiced mask + ranges.  ranges: f32[nr*rs] with nr = ceil(n/rs); mask_out: optional u8[n].
+int fwav_voiced_ranges(const float* sig, int64_t n, int rs, int frame, int smooth_window, float hi, float lo,
+                       float* ranges, int64_t nr, uint8_t* mask_out, void* workspace, size_t ws_bytes,
+                       void* stream) {
+  FWAV_CHECK_ARG(sig && ranges && n > 0 && rs > 0 && frame > 0, FWAV_ERR_ARG, "fwav_voiced_ranges: bad args");
+  FWAV_CHECK_ARG(nr == cdiv(n, rs), FWAV_ERR_SHAPE, "fwav_voiced_ranges: nr != ceil(n/rs)");
+  FWAV_CHECK_ARG(frame <= kMaxPairwise, FWAV_ERR_SHAPE, "fwav_voiced_ranges: frame > %d", kMaxPairwise);
+  const int64_t nf = cdiv(n, frame);
+  FWAV_CHECK_ARG(smooth_window >= 1 && smooth_window <= 11 && nf >= smooth_window, FWAV_ERR_SHAPE,
+                 "fwav_voiced_ranges: need 1 <= smooth_window <= 11 and n_frames >= smooth_window");
+  FWAV_CHECK_ARG(ws_bytes >= fwav_voiced_workspace_size(n, frame), FWAV_ERR_WORKSPACE,
+                 "fwav_voiced_ranges: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nb = cdiv(nf, kFramesPerBlock);
+  char* w = (char*)workspace;
+  int64_t* blast = (int64_t*)w;
+  int64_t* carry = blast + nb;
+  float* energy = (float*)(carry + nb);
+  int8_t* dec = (int8_t*)(energy + nf);
+  uint8_t* state = (uint8_t*)(dec + nf);
+  // smoothing kernel weights: np.ones(w, f32) / w
+  const float kw = 1.0f / (float)smooth_window;
+  k_frame_energy<<<cdiv(nf, kSignalThreads), kSignalThreads, 0, st>>>(sig, n, frame, nf, energy);
+  k_voiced_decide<<<nb, kSignalThreads, 0, st>>>(energy, nf, smooth_window, kw, hi, lo, dec, blast);
+  k_voiced_carry<<<1, 1024, 0, st>>>(blast, nb, carry);
+  k_frame_state<<<nb, kSignalThreads, 0, st>>>(dec, carry, nf, state);
+  const int64_t total = nr * rs;
+  k_form_ranges<<<cdiv(total, kSignalThreads), kSignalThreads, 0, st>>>(sig, n, frame, state, total, ranges,
+                                                                          mask_out);
+  FWAV_LAUNCH_CHECK("fwav_voiced_ranges");
+  return FWAV_OK;
+}
+
+// Block partials of Σ ranges[0:n]² (f64), `nblocks` of them; the host sums them in order.
+int fwav_weighted_energy(const float* ranges, int64_t n, double* partial, int nblocks, void* stream) {
+  FWAV_CHECK_ARG(ranges && partial && n >= 0 && nblocks > 0, FWAV_ERR_ARG, "fwav_weighted_energy: bad args");
+  k_weighted_energy<<<nblocks, kSignalThreads, 0, (hipStream_t)stream>>>(ranges, n, partial);
+  FWAV_LAUNCH_CHECK("fwav_weighted_energy");
+  return FWAV_OK;
+}
+
+// Ranges [q_offset, q_offset + nr) of the whole signal: ranges/cand/active are shard-local (row i), the
+// query embedding of local range i is emb row q_offset + i.
+int fwav_prune(const float* ranges, int64_t nr, int64_t q_offset, int rs, float prune_thr, int fast_mode,
+               const float* emb, int64_t nd, int k, int32_t* cand, int32_t* active, int32_t* n_active, void* stream) {
+  FWAV_CHECK_ARG(ranges && emb && cand && active && n_active && k > 0, FWAV_ERR_ARG, "fwav_prune: bad args");
+  FWAV_CHECK_ARG(q_offset >= 0 && q_offset + nr <= nd, FWAV_ERR_SHAPE,
+                 "fwav_prune: query rows past n_domains (query rows are domain rows, quirk Q1)");
+  FWAV_CHECK_ARG(rs <= kMaxPairwise, FWAV_ERR_SHAPE, "fwav_prune: rs too large");
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(n_active, 0, sizeof(int32_t), st);
+  if (nr == 0) return FWAV_OK;
+  k_prune<<<cdiv(nr, kSignalThreads), kSignalThreads, 0, st>>>(ranges, nr, q_offset, rs, prune_thr, fast_mode, emb,
+                                                                nd, k, cand, active, n_active);
+  FWAV_LAUNCH_CHECK("fwav_prune");
+  return FWAV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+"""ctypes binding of ``libfwav.so`` — the C-ABI boundary declared in ``include/fwav.h``.
+
+The product path has no CPU fallback: if the library (built by ``__graft_entry__.build()``) is missing or
+no HIP device is visible, every entry point raises :class:`FwavError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfwav.so")
+
+P = C.c_void_p
+I64 = C.c_int64
+I32 = C.c_int
+F32 = C.c_float
+F64 = C.c_double
+SZ = C.c_size_t
+
+#: name → (restype, argtypes); must match include/fwav.h exactly (tests/test_capi.py checks the header).
+SIGNATURES = {
+    "fwav_last_error": (C.c_char_p, []),
+    "fwav_abi_version": (I32, []),
+    "fwav_stream_sync": (I32, [P]),
+    "fwav_voiced_workspace_size": (SZ, [I64, I32]),
+    "fwav_voiced_ranges": (I32, [P, I64, I32, I32, I32, F32, F32, P, I64, P, P, SZ, P]),
+    "fwav_weighted_energy": (I32, [P, I64, P, I32, P]),
+    "fwav_prune": (I32, [P, I64, I64, I32, F32, I32, P, I64, I32, P, P, P, P]),
+    "fwav_embed_tables": (I32, [I32, P]),
+    "fwav_pool_workspace_size": (SZ, [I64, I32, I32, I32]),
+    "fwav_pool_embed": (I32, [P, I64, I32, I32, I32, P, P, P, P, SZ, P]),
+    "fwav_topk_max_k": (I32, []),
+    "fwav_sim_topk": (I32, [P, I64, P, P, I64, I64, I32, P, P]),
+    "fwav_affine": (I32, [P, I64, I32, P, I32, P, I64, F32, P, P, P, P, P, P]),
+    "fwav_decode_workspace_size": (SZ, [I64, I32, I32]),
+    "fwav_decode": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, SZ, P]),
+}
+
+
+class FwavError(RuntimeError):
+    """A C-ABI call returned a non-zero status (message from ``fwav_last_error``)."""
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FwavError(f"HIP library not built: {LIB_PATH} is missing (run __graft_entry__.build())")
+        dll = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(dll, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = dll
+    return _lib
+
+
+def call(name: str, *args) -> int:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().fwav_last_error().decode(errors="replace")
+        raise FwavError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def size_call(name: str, *args) -> int:
+    return int(getattr(lib(), name)(*args))

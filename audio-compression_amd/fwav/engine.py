@@ -1,0 +1,228 @@
+"""Device pipeline: the hot path of ``compress_audio`` / ``decompress_audio`` on one MI355X.
+
+Everything between the input signal and the match arrays stays in HBM and runs on one HIP stream through
+the C-ABI of ``libfwav.so`` (``include/fwav.h``); torch only provides device memory and the stream.  There
+is no CPU fallback: without the library or a device every call raises :class:`~fwav._lib.FwavError`.
+
+Reference map (``/root/reference/fractal.py``):
+  voiced_detection :880-909 + range formation :1074-1112  → fwav_voiced_ranges
+  silent-input test :1083                                  → fwav_weighted_energy (f64 partials)
+  build_domains_memmap :285-334 + build_domain_embeddings :238-280 → fwav_pool_embed
+  cpu_worker energy prune :601-603, pad :622               → fwav_prune
+  linear top-K :535-541, 617-620                           → fwav_sim_topk
+  _process_gpu_batch :757-850                              → fwav_affine
+  decompress_audio :1378-1473                              → fwav_decode
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import FwavError, call, size_call
+
+F32 = np.float32
+
+
+def geometry(tile_size: int) -> tuple[int, int]:
+    """range_size, domain_step (fractal.py:1070-1071)."""
+    rs = max(4, tile_size // 256)
+    return rs, max(1, rs // 4)
+
+
+def n_domains_for(n: int, tile_size: int, step: int) -> int:
+    return 0 if n < tile_size else (n - tile_size) // step + 1
+
+
+def require_device(device=None) -> torch.device:
+    _lib.lib()
+    if not torch.cuda.is_available():
+        raise FwavError("no HIP device visible: the fwav engine has no CPU path")
+    return torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+_TABLES: dict = {}
+
+
+def embed_tables(rs: int, device: torch.device) -> torch.Tensor:
+    key = (rs, str(device))
+    if key not in _TABLES:
+        host = np.zeros(16 * rs, np.float64)
+        call("fwav_embed_tables", rs, host.ctypes.data)
+        _TABLES[key] = torch.from_numpy(host).to(device)
+    return _TABLES[key]
+
+
+@dataclasses.dataclass
+class DeviceCompressed:
+    """Result of :func:`compress_device`.  Device tensors; ``finalize()`` synchronises once."""
+
+    n_ranges: int
+    range_size: int
+    tile_size: int
+    domain_step: int
+    energy_thresh: float
+    original_len: int
+    n_domains: int
+    top_k: int
+    shard: tuple[int, int]
+    ranges: Optional[torch.Tensor] = None
+    pool: Optional[torch.Tensor] = None
+    emb: Optional[torch.Tensor] = None
+    cand: Optional[torch.Tensor] = None
+    idx: Optional[torch.Tensor] = None
+    s: Optional[torch.Tensor] = None
+    o: Optional[torch.Tensor] = None
+    sym: Optional[torch.Tensor] = None
+    err: Optional[torch.Tensor] = None
+    n_active: Optional[torch.Tensor] = None
+    energy_partial: Optional[torch.Tensor] = None
+    empty: bool = False
+
+    def is_silent(self) -> bool:
+        """Σ(signal·mask)² < 1e-8 (fractal.py:1083); f64 here, f32 pairwise in the reference."""
+        if self.energy_partial is None:
+            return True
+        return float(np.sum(self.energy_partial.cpu().numpy())) < 1e-8
+
+
+def _mark(ev, name: str, end: bool = False):
+    """Record a HIP event on the current stream into ev[name] = [start, end] (bench instrumentation)."""
+    if ev is None:
+        return
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    ev.setdefault(name, []).append(e)
+
+
+def _empty(n, rs, tile, step, thr, k) -> DeviceCompressed:
+    return DeviceCompressed(0, rs, tile, step, thr, n, 0, k, (0, 0), empty=True)
+
+
+def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh: float = 1e-4,
+                    fast_mode: bool = True, s_clip: float = 16.0, shard: Optional[tuple[int, int]] = None,
+                    keep_intermediates: bool = False, events: Optional[dict] = None) -> DeviceCompressed:
+    """Run the compress hot path on ``sig`` (1-D float32 tensor on a HIP device).
+
+    ``shard=(lo, hi)`` restricts candidate search and the affine solve to ranges ``[lo, hi)`` (the
+    multi-GPU path); voiced detection, pool and embeddings are always computed for the whole signal,
+    because query vectors are domain-embedding rows (quirk Q1) and the voiced state is a scan over the
+    whole signal.  Raises ValueError for the reference's own error cases (empty input; n_ranges >
+    n_domains).
+    """
+    if sig.dim() != 1 or sig.dtype != torch.float32 or not sig.is_cuda:
+        raise ValueError("compress_device expects a 1-D float32 device tensor")
+    dev = sig.device
+    st = _stream(dev)
+    sig = sig.contiguous()
+    n = sig.numel()
+    k = int(top_k)
+    rs, step = geometry(tile_size)
+    frame = 2 * rs
+    if n == 0:
+        raise ValueError("a cannot be empty")  # np.convolve on zero frames (fractal.py:895)
+    nf = -(-n // frame)
+    nr = -(-n // rs)
+    nd = n_domains_for(n, tile_size, step)
+    if nf < 5:
+        # every such input is shorter than the tile for tile >= 40 → the reference's empty result
+        if n < tile_size and tile_size >= 40:
+            return _empty(n, rs, tile_size, step, energy_thresh, k)
+        raise NotImplementedError("inputs shorter than 5 voiced-detection frames need tile_size >= 40")
+    thr32 = F32(energy_thresh)
+    lo32 = F32(energy_thresh * 0.5)
+    if k > size_call("fwav_topk_max_k"):
+        raise NotImplementedError(f"top_k={k} > {size_call('fwav_topk_max_k')} is not supported by the HIP search")
+    ws_n = size_call("fwav_voiced_workspace_size", n, frame)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+    ranges = torch.empty(nr * rs, dtype=torch.float32, device=dev)
+    _mark(events, "voiced_ranges")
+    call("fwav_voiced_ranges", sig.data_ptr(), n, rs, frame, 5, float(thr32), float(lo32), ranges.data_ptr(), nr,
+         None, ws.data_ptr(), ws_n, st)
+    partial = torch.empty(256, dtype=torch.float64, device=dev)
+    call("fwav_weighted_energy", ranges.data_ptr(), n, partial.data_ptr(), 256, st)
+    _mark(events, "voiced_ranges")
+    res = DeviceCompressed(nr, rs, tile_size, step, energy_thresh, n, nd, k, (0, nr), energy_partial=partial)
+    if n < tile_size or nr > nd:
+        # the reference returns the empty tuple for silent input before it ever builds domains
+        if res.is_silent() or n < tile_size:
+            return _empty(n, rs, tile_size, step, energy_thresh, k)
+        raise ValueError("mmap length is greater than file size")  # quirk Q9 (fractal.py:1190-1195)
+    lo, hi = (0, nr) if shard is None else (int(shard[0]), int(shard[1]))
+    if not (0 <= lo <= hi <= nr):
+        raise ValueError(f"bad shard {shard} for {nr} ranges")
+    res.shard = (lo, hi)
+    tab = embed_tables(rs, dev)
+    pool = torch.empty(nd * rs, dtype=torch.float32, device=dev)
+    emb = torch.empty(nd * 16, dtype=torch.float32, device=dev)
+    ws_p = size_call("fwav_pool_workspace_size", n, tile_size, rs, step)
+    wsp = torch.empty(max(ws_p, 16), dtype=torch.uint8, device=dev)
+    _mark(events, "pool_embed")
+    call("fwav_pool_embed", sig.data_ptr(), n, tile_size, rs, step, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
+         wsp.data_ptr(), ws_p, st)
+    _mark(events, "pool_embed")
+    m = hi - lo
+    cand = torch.empty(max(m, 1) * k, dtype=torch.int32, device=dev)
+    active = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+    n_active = torch.empty(1, dtype=torch.int32, device=dev)
+    rsh = ranges[lo * rs:hi * rs]
+    idx = torch.empty(m, dtype=torch.int32, device=dev)
+    s = torch.empty(m, dtype=torch.float32, device=dev)
+    o = torch.empty(m, dtype=torch.float32, device=dev)
+    sym = torch.empty(m, dtype=torch.uint8, device=dev)
+    err = torch.empty(m, dtype=torch.float32, device=dev)
+    if m > 0:
+        _mark(events, "prune")
+        call("fwav_prune", rsh.data_ptr(), m, lo, rs, float(F32(energy_thresh * 0.75)), int(bool(fast_mode)),
+             emb.data_ptr(), nd, k, cand.data_ptr(), active.data_ptr(), n_active.data_ptr(), st)
+        _mark(events, "prune")
+        _mark(events, "sim_topk")
+        call("fwav_sim_topk", emb.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), m, lo, k, cand.data_ptr(), st)
+        _mark(events, "sim_topk")
+        _mark(events, "affine")
+        call("fwav_affine", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd,
+             float(abs(F32(s_clip))), idx.data_ptr(), s.data_ptr(), o.data_ptr(), sym.data_ptr(), err.data_ptr(), st)
+        _mark(events, "affine")
+    res.pool, res.idx, res.s, res.o, res.sym, res.err, res.n_active = pool, idx, s, o, sym, err, n_active
+    if keep_intermediates:
+        res.ranges, res.emb, res.cand = ranges, emb, cand
+    return res
+
+
+def decompress_device(idx: torch.Tensor, s: torch.Tensor, o: torch.Tensor, sym: torch.Tensor, pool: torch.Tensor,
+                      n_ranges: int, range_size: int, iterations: int = 8, convergence_eps: float = 1e-3,
+                      s_clip: float = 16.0, s_damping: float = 0.0):
+    """decompress_audio's loop on device.  Returns (recon f32[n_ranges*range_size] tensor, iterations_run,
+    deltas f64 list).  One host synchronisation (to read the iteration count)."""
+    dev = idx.device
+    st = _stream(dev)
+    nr, rs = int(n_ranges), int(range_size)
+    nd = pool.numel() // rs if rs > 0 else 0
+    it = int(iterations)
+    a = torch.empty(max(nr * rs, 1), dtype=torch.float32, device=dev)
+    b = torch.empty(max(nr * rs, 1), dtype=torch.float32, device=dev)
+    deltas = torch.zeros(max(it, 1), dtype=torch.float64, device=dev)
+    state = torch.zeros(2, dtype=torch.int32, device=dev)
+    wsn = size_call("fwav_decode_workspace_size", nr, rs, it)
+    ws = torch.empty(max(wsn, 16), dtype=torch.uint8, device=dev)
+    call("fwav_decode", idx.data_ptr(), s.data_ptr(), o.data_ptr(), sym.data_ptr(), nr, rs, pool.data_ptr(), nd, it,
+         float(convergence_eps), float(abs(F32(s_clip))), float(s_damping), a.data_ptr(), b.data_ptr(),
+         deltas.data_ptr(), state.data_ptr(), ws.data_ptr(), wsn, st)
+    stt = state.cpu().numpy()
+    ran = int(stt[1])
+    out = b if (ran % 2 == 1) else a
+    if nr == 0:
+        out = a[:0]
+    return out[:nr * rs], ran, deltas.cpu().numpy()[:ran].tolist()
