@@ -58,7 +58,8 @@ __global__ void k_domain_pool(const float* __restrict__ sig, int64_t nd, int rs,
 //   tab layout (f64): tonal rows [8][rs] then transient rows [8][rs]; zero rows past take / tk.
 template <int RS>
 __global__ void k_embed(const float* __restrict__ src, int64_t nd, int rs, int64_t a, int64_t b,
-                        const double* __restrict__ tab, float* __restrict__ pool_out, float* __restrict__ emb) {
+                        const double* __restrict__ tab, float* __restrict__ pool_out, float* __restrict__ emb,
+                        _Float16* __restrict__ emb16) {
   int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= nd) return;
   const int n = RS > 0 ? RS : rs;
@@ -142,12 +143,24 @@ __global__ void k_embed(const float* __restrict__ src, int64_t nd, int rs, int64
   float4* o4 = reinterpret_cast<float4*>(emb + d * 16);
 #pragma unroll
   for (int j = 0; j < 4; ++j) o4[j] = make_float4(out[4 * j], out[4 * j + 1], out[4 * j + 2], out[4 * j + 3]);
+  if (emb16 != nullptr) {
+    // fp16 copy for the similarity pre-filter, tiled [chunk of 256][half h][256][8] (fwav_topk.hip)
+    const int64_t c = d >> 8, j = d & 255;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+      half8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (_Float16)out[8 * hh + e];
+      *reinterpret_cast<half8*>(emb16 + ((c * 2 + hh) * 256 + j) * 8) = v;
+    }
+  }
 }
 
 template <int RS>
 static void launch_embed(const float* src, int64_t nd, int rs, int64_t a, int64_t b, const double* tab,
-                         float* pool_out, float* emb, hipStream_t st) {
-  k_embed<RS><<<cdiv(nd, kPoolThreads), kPoolThreads, 0, st>>>(src, nd, rs, a, b, tab, pool_out, emb);
+                         float* pool_out, float* emb, _Float16* emb16, hipStream_t st) {
+  k_embed<RS><<<cdiv(nd, kPoolThreads), kPoolThreads, 0, st>>>(src, nd, rs, a, b, tab, pool_out, emb, emb16);
 }
 
 }  // namespace fwav
@@ -184,8 +197,10 @@ size_t fwav_pool_workspace_size(int64_t n, int tile, int rs, int step) {
 }
 
 // Domain pool + embedding.  pool: f32[nd*rs], emb: f32[nd*16], tab: device copy of fwav_embed_tables(rs).
+// emb16 (optional): fp16 copy in the tiled layout the similarity search streams,
+// f16[ceil(nd/256)*256*16]; rows past nd are zeroed here.
 int fwav_pool_embed(const float* sig, int64_t n, int tile, int rs, int step, const double* tab, float* pool,
-                    float* emb, void* workspace, size_t ws_bytes, void* stream) {
+                    float* emb, void* emb16, void* workspace, size_t ws_bytes, void* stream) {
   FWAV_CHECK_ARG(sig && pool && emb && tab && tile > 0 && rs > 0 && step > 0, FWAV_ERR_ARG,
                  "fwav_pool_embed: bad args");
   FWAV_CHECK_ARG(n >= tile, FWAV_ERR_SHAPE, "fwav_pool_embed: n < tile");
@@ -212,11 +227,18 @@ int fwav_pool_embed(const float* sig, int64_t n, int tile, int rs, int step, con
     k_domain_pool<<<cdiv(nd * rs, kPoolThreads), kPoolThreads, 0, st>>>(sig, nd, rs, step, bl, pool);
     src = pool; a = rs; b = 1; pool_out = nullptr;
   }
+  _Float16* e16 = (_Float16*)emb16;
+  if (e16 != nullptr && (nd & 255) != 0) {
+    // zero the padded tail of the last chunk (both halves)
+    const int64_t c = nd >> 8, j0 = nd & 255;
+    for (int hh = 0; hh < 2; ++hh)
+      (void)hipMemsetAsync(e16 + ((c * 2 + hh) * 256 + j0) * 8, 0, (size_t)(256 - j0) * 8 * sizeof(_Float16), st);
+  }
   switch (rs) {
-    case 4: launch_embed<4>(src, nd, rs, a, b, tab, pool_out, emb, st); break;
-    case 8: launch_embed<8>(src, nd, rs, a, b, tab, pool_out, emb, st); break;
-    case 16: launch_embed<16>(src, nd, rs, a, b, tab, pool_out, emb, st); break;
-    default: launch_embed<0>(src, nd, rs, a, b, tab, pool_out, emb, st); break;
+    case 4: launch_embed<4>(src, nd, rs, a, b, tab, pool_out, emb, e16, st); break;
+    case 8: launch_embed<8>(src, nd, rs, a, b, tab, pool_out, emb, e16, st); break;
+    case 16: launch_embed<16>(src, nd, rs, a, b, tab, pool_out, emb, e16, st); break;
+    default: launch_embed<0>(src, nd, rs, a, b, tab, pool_out, emb, e16, st); break;
   }
   FWAV_LAUNCH_CHECK("fwav_pool_embed");
   return FWAV_OK;

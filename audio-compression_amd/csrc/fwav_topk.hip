@@ -222,23 +222,321 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
   }
 }
 
+// ------------------------------------------------------------------ fp16 pre-filter + exact f32 rescoring
+// Same contract and results as k_sim_topk_f32.  Scores are first formed by ONE v_mfma_f32_32x32x16_f16 per
+// 32×32 tile from the fp16 copy of the table (vs eight f32 MFMAs).  |s16 − s32| ≤ 2u·‖q‖‖d‖ + f32
+// accumulation error ≤ 1.96e-3 (u = 2^-11, ‖q‖, ‖d‖ ≤ √2), so with δ = 2.5e-3 every domain with
+// s16 ≤ θ − δ has s32 < θ, where θ is the EXACT f32 score of the current K-th best: it cannot enter the
+// top-K and is skipped.  Survivors are appended by index only; when a buffer fills, the wave rescores the
+// not-yet-exact entries in f32 (the f32 MFMA's fma order, k = 0..15; one lane per entry, all loads in
+// flight together), sorts, keeps the top K and sets θ.  Because skipped domains are strictly below θ the
+// result is the exact (score desc, index asc) top-K whatever the processing order.
+//
+// Geometry: 8 waves × 32 queries per workgroup; the per-query key buffers (C × 8 B) live in a global
+// workspace (touched only on the rare slow path, L2/MALL-resident), so LDS holds just two 8 KB chunk
+// slots + per-query counters (≈ 21 KB) and a CU runs two workgroups = 4 waves per SIMD.  Per chunk (256
+// domains; kGroup chunks per barrier, prefetched a group ahead in registers) each wave issues 8 MFMAs,
+// reduces each tile to its per-lane max (max3 tree) and takes ONE ballot; only when some lane clears
+// θ − δ does it call the out-of-line slow path.
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+constexpr float kF16Delta = 2.5e-3f;
+
+// Diagnostic counters (fwav_debug_sim_topk only; stays nullptr in production launches):
+//   [0] slow_chunk calls  [1] firing tiles  [2] appends  [3] compactions
+//   [4] cycles in slow_chunk  [5] cycles in compactions  [6] cycles per wave (whole kernel)
+__device__ unsigned long long* g_topk_stats = nullptr;
+__device__ __forceinline__ void stat_add(int i, unsigned long long v) {
+  if (g_topk_stats != nullptr && (threadIdx.x & 63) == 0) atomicAdd(g_topk_stats + i, v);
+}
+constexpr int kGroup = 4;            // chunks per barrier (and per register prefetch group)
+constexpr int k16Waves = 8;
+constexpr int k16Q = 32 * k16Waves;  // queries per workgroup
+constexpr int k16Threads = 64 * k16Waves;
+constexpr int k16Cap = 256;          // key-buffer entries per query (global workspace)
+
+__device__ __forceinline__ float score32(const float* __restrict__ emb, int64_t d, const float (&q)[16]) {
+  const float4* p = reinterpret_cast<const float4*>(emb + d * 16);
+  float acc = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float4 v = p[j];
+    acc = __builtin_fmaf(v.x, q[4 * j + 0], acc);
+    acc = __builtin_fmaf(v.y, q[4 * j + 1], acc);
+    acc = __builtin_fmaf(v.z, q[4 * j + 2], acc);
+    acc = __builtin_fmaf(v.w, q[4 * j + 3], acc);
+  }
+  return acc;
+}
+
+// Max of the 16 scores of a lane as an int over the float bits (v_max3_i32; a float max would be preceded
+// by canonicalising v_max_f32 x,x on every MFMA output).  For a threshold t >= 0, (int)x > (int)t ⟺ x > t
+// for every non-NaN x (negative floats are negative ints); callers use it only in that regime.
+__device__ __forceinline__ int imax16(const floatx16& a) {
+  auto I = [&](int i) { return __float_as_int(a[i]); };
+  auto mx = [](int x, int y) { return x > y ? x : y; };
+  const int m0 = mx(mx(I(0), I(1)), I(2));
+  const int m1 = mx(mx(I(3), I(4)), I(5));
+  const int m2 = mx(mx(I(6), I(7)), I(8));
+  const int m3 = mx(mx(I(9), I(10)), I(11));
+  const int m4 = mx(mx(I(12), I(13)), I(14));
+  return mx(mx(mx(m0, m1), mx(m2, m3)), mx(m4, I(15)));
+}
+
+// Does any score in this lane's imax beat the filter thf?  Exact for thf >= 0; always true for thf < 0
+// (then the exact per-score test in the slow path decides).
+__device__ __forceinline__ bool may_pass(int imx, float thf) {
+  return thf < 0.0f || imx > __float_as_int(thf);
+}
+
+struct Topk16Smem {
+  int cnt[k16Q];      // entries in the query's buffer
+  int nex[k16Q];      // leading entries that are exact (sorted top-K after the last compaction)
+  float theta[k16Q];  // exact K-th score (−inf until K entries)
+  int64_t qrow[k16Q];
+};
+
+// Rescore the inexact tail of query ql's buffer kq[0..C), sort, keep the top K, set θ.  Whole wave.
+// Every per-query buffer and counter is owned by one wave, so no cross-wave fences are needed; the wave's
+// own appended stores are drained once (vmcnt(0)), then all key loads and all row loads are issued
+// together (two memory round trips in total).
+template <int C>
+__device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, Topk16Smem& sm, int ql, int K,
+                                          const float* __restrict__ emb) {
+  constexpr int E = C / 64;
+  const unsigned long long t_start = g_topk_stats ? __builtin_amdgcn_s_memtime() : 0;
+  const int lane = threadIdx.x & 63;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int n = sm.cnt[ql];
+  const int ne = sm.nex[ql];
+  const float4* qp = reinterpret_cast<const float4*>(emb + sm.qrow[ql] * 16);
+  uint64_t v[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    v[j] = e < n ? kq[e] : 0ull;
+  }
+  float qv[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 w = qp[i];
+    qv[4 * i] = w.x; qv[4 * i + 1] = w.y; qv[4 * i + 2] = w.z; qv[4 * i + 3] = w.w;
+  }
+  // rescore the inexact entries two slots at a time (8 row loads in flight per lane)
+#pragma unroll
+  for (int j0 = 0; j0 < E; j0 += 2) {
+    float4 row[2][4];
+    int32_t dd[2];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = j0 + jj;
+      const int e = j * 64 + lane;
+      dd[jj] = (j < E && e >= ne && e < n) ? (int32_t)(uint32_t)v[j < E ? j : 0] : 0;
+      const float4* p = reinterpret_cast<const float4*>(emb + (int64_t)dd[jj] * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) row[jj][i] = p[i];
+    }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = j0 + jj;
+      const int e = j * 64 + lane;
+      if (j < E && e >= ne && e < n) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc = __builtin_fmaf(row[jj][i].x, qv[4 * i + 0], acc);
+          acc = __builtin_fmaf(row[jj][i].y, qv[4 * i + 1], acc);
+          acc = __builtin_fmaf(row[jj][i].z, qv[4 * i + 2], acc);
+          acc = __builtin_fmaf(row[jj][i].w, qv[4 * i + 3], acc);
+        }
+        v[j] = make_key(acc, dd[jj]);
+      }
+    }
+  }
+  wave_sort_desc<E>(v);
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    if (e < K && e < n) kq[e] = v[j];
+  }
+  const int kl = (K - 1) & 63, kj = (K - 1) >> 6;
+  uint64_t kth = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j)
+    if (j == kj) kth = __shfl(v[j], kl);
+  if (lane == 0) {
+    const int m = n < K ? n : K;
+    sm.cnt[ql] = m;
+    sm.nex[ql] = m;
+    sm.theta[ql] = n >= K ? key_score(kth) : -INFINITY;
+  }
+  if (g_topk_stats) {
+    stat_add(3, 1);
+    stat_add(5, __builtin_amdgcn_s_memtime() - t_start);
+  }
+}
+
+// Slow path for one chunk (inline; taken when some lane's tile max clears θ − δ): recompute each tile's
+// MFMA from the LDS slot, append the survivors' indices to the wave-owned global key buffers (one LDS
+// atomic per lane per tile reserves the slot range), compact full buffers.  Returns the new θ − δ.
+template <int C>
+__device__ __forceinline__ float slow_chunk(const _Float16* __restrict__ lda, half8 b, float thf, int64_t dbase,
+                                            int64_t nd, uint64_t* __restrict__ gkeys, Topk16Smem& sm, int K,
+                                            const float* __restrict__ emb, int upd) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int col = lane & 31;
+  const int h = lane >> 5;
+  const int ql = wave * 32 + col;
+  uint64_t* kq = gkeys + (size_t)ql * C;
+  stat_add(0, 1);
+  for (int t = 0; t < 8; ++t) {
+    const half8 a = *reinterpret_cast<const half8*>(lda + ((h * kChunk) + t * 32 + col) * 8);
+    const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, floatx16{}, 0, 0, 0);
+    const int64_t d0 = dbase + t * 32 + 4 * h;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t d = d0 + (r & 3) + 8 * (r >> 2);
+      mask |= (acc[r] > thf && d < nd) ? (1u << r) : 0u;
+    }
+    if (__ballot(mask != 0u) == 0ull) continue;
+    stat_add(1, 1);
+    const int cntm = __builtin_popcount(mask);
+    int base = 0;
+    if (cntm) base = atomicAdd(&sm.cnt[ql], cntm);
+    while (mask) {
+      const int r = __builtin_ctz(mask);
+      mask &= mask - 1;
+      kq[base++] = (uint64_t)(uint32_t)(d0 + (r & 3) + 8 * (r >> 2));
+    }
+    if (g_topk_stats && cntm) atomicAdd(g_topk_stats + 2, (unsigned long long)cntm);
+    uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > C - 32);
+    while (need != 0ull) {
+      const int l = __builtin_ctzll(need);
+      need &= need - 1;
+      compact16<C>(gkeys + (size_t)(wave * 32 + l) * C, sm, wave * 32 + l, K, emb);
+    }
+    if (upd) thf = sm.theta[ql] - kF16Delta;
+  }
+  return thf;
+}
+
+template <int C>
+__global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
+                                                                const float* __restrict__ emb, int64_t nd,
+                                                                const int32_t* __restrict__ active,
+                                                                const int32_t* __restrict__ n_active_p,
+                                                                int64_t q_offset, int K, int32_t* __restrict__ cand,
+                                                                uint64_t* __restrict__ gkeys_all, int dbg) {
+  // 2 × kGroup chunk slots: a group of kGroup chunks is written, one barrier, then consumed; the next
+  // group goes to the other half, so waves may drift up to a group apart between barriers.
+  __shared__ __attribute__((aligned(16))) uint4 slots[2 * kGroup][512];
+  __shared__ Topk16Smem sm;
+
+  const int n_active = *n_active_p;
+  const int qbase = blockIdx.x * k16Q;
+  if (qbase >= n_active) return;
+  uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * k16Q * C;
+  const unsigned long long t_kernel = g_topk_stats ? __builtin_amdgcn_s_memtime() : 0;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int col = lane & 31;
+  const int h = lane >> 5;
+  const int ql = wave * 32 + col;
+  const int qi = qbase + ql;
+  const int32_t q = qi < n_active ? active[qi] : -1;
+  const int64_t qrow = (int64_t)(q < 0 ? 0 : q) + q_offset;
+  const half8 b = *reinterpret_cast<const half8*>(emb16 + (((qrow >> 8) * 2 + h) * 256 + (qrow & 255)) * 8);
+  // dbg (diagnostic ablations, timing only — outputs are wrong when set):
+  //   1 = never take the slow path, 2 = skip MFMA + threshold test, 4 = no global chunk loads
+  const int upd = (q >= 0 && !(dbg & 1)) ? 1 : 0;
+  float thf = upd ? -INFINITY : INFINITY;
+  if (h == 0) {
+    sm.cnt[ql] = 0;
+    sm.nex[ql] = 0;
+    sm.theta[ql] = -INFINITY;
+    sm.qrow[ql] = qrow;
+  }
+
+  const int64_t nchunks = cdiv(nd, kChunk);
+  const int64_t ngroups = cdiv(nchunks, kGroup);
+  const uint4* src = reinterpret_cast<const uint4*>(emb16);
+  uint4 pf[kGroup];
+  auto load_group = [&](int64_t g) {
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      const int64_t c = g * kGroup + j;
+      pf[j] = (c < nchunks && !(dbg & 4)) ? src[c * 512 + tid] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  load_group(0);
+
+  for (int64_t g = 0; g < ngroups; ++g) {
+    uint4(*half)[512] = slots + (g & 1) * kGroup;
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) half[j][tid] = pf[j];
+    if (g + 1 < ngroups) load_group(g + 1);
+    __syncthreads();
+    if (dbg & 2) continue;
+    const int64_t c_end = (g + 1) * kGroup < nchunks ? (g + 1) * kGroup : nchunks;
+    for (int64_t c = g * kGroup; c < c_end; ++c) {
+      const _Float16* lda = reinterpret_cast<const _Float16*>(half[c - g * kGroup]);
+      int m[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const half8 a = *reinterpret_cast<const half8*>(lda + ((h * kChunk) + t * 32 + col) * 8);
+        m[t] = imax16(__builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, floatx16{}, 0, 0, 0));
+      }
+      auto mx = [](int x, int y) { return x > y ? x : y; };
+      const int mall = mx(mx(mx(m[0], m[1]), mx(m[2], m[3])), mx(mx(m[4], m[5]), mx(m[6], m[7])));
+      if (__ballot(may_pass(mall, thf)) != 0ull)
+        thf = slow_chunk<C>(lda, b, thf, c * kChunk, nd, gkeys, sm, K, emb, upd);
+    }
+  }
+
+  for (int l = 0; l < 32; ++l) {
+    const int qs = wave * 32 + l;
+    const int qq = qbase + qs;
+    if (qq >= n_active) break;
+    const int32_t qid = active[qq];
+    uint64_t* kq = gkeys + (size_t)qs * C;
+    compact16<C>(kq, sm, qs, K, emb);
+    const int n = sm.cnt[qs];
+    int32_t* out = cand + (int64_t)qid * K;
+    for (int e = lane; e < K; e += 64) out[e] = e < n ? key_idx(kq[e]) : -1;
+  }
+  if (g_topk_stats) stat_add(6, __builtin_amdgcn_s_memtime() - t_kernel);
+}
+
 template <int C>
 static size_t topk_lds_bytes() {
   return (size_t)kTopkQ * C * sizeof(uint64_t) + 16 * kChunk * sizeof(float) + 2 * kTopkQ * sizeof(int);
 }
 
 template <int C>
-static int launch_topk(const float* emb, int64_t nd, const int32_t* active, const int32_t* n_active, int64_t max_q,
-                       int64_t q_offset, int K, int32_t* cand, hipStream_t st) {
-  const size_t lds = topk_lds_bytes<C>();
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_sim_topk_f32<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
+static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, const int32_t* active,
+                       const int32_t* n_active, int64_t max_q, int64_t q_offset, int K, int32_t* cand, hipStream_t st,
+                       uint64_t* gkeys, int dbg = 0) {
   const int64_t grid = cdiv(max_q, kTopkQ);
   if (grid == 0) return FWAV_OK;
-  k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, active, n_active, q_offset, K, cand);
+  if (emb16 != nullptr) {
+    if (gkeys == nullptr) {
+      set_error("fwav_sim_topk: fp16 search needs its key workspace (fwav_sim_topk_workspace_size)");
+      return FWAV_ERR_WORKSPACE;
+    }
+    k_sim_topk_f16<k16Cap><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(emb16, emb, nd, active, n_active, q_offset, K,
+                                                                       cand, gkeys, dbg);
+  } else {
+    const size_t lds = topk_lds_bytes<C>();
+    static bool attr32 = false;
+    if (!attr32) {
+      (void)hipFuncSetAttribute((const void*)k_sim_topk_f32<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr32 = true;
+    }
+    k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, active, n_active, q_offset, K, cand);
+  }
   FWAV_LAUNCH_CHECK("fwav_sim_topk");
   return FWAV_OK;
 }
@@ -251,16 +549,41 @@ extern "C" {
 
 int fwav_topk_max_k(void) { return 64; }
 
+// Global key-buffer workspace of the fp16 search for up to max_q queries (bytes).
+size_t fwav_sim_topk_workspace_size(int64_t max_q) {
+  return (size_t)cdiv(max_q > 0 ? max_q : 1, k16Q) * k16Q * k16Cap * sizeof(uint64_t);
+}
+
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,
 // at most max_q); local query i uses embedding row q_offset + i and writes cand row i.  Rows of queries
-// not listed are not touched.
-int fwav_sim_topk(const float* emb, int64_t nd, const int32_t* active, const int32_t* n_active, int64_t max_q,
-                  int64_t q_offset, int K, int32_t* cand, void* stream) {
+// not listed are not touched.  emb16 (tiled fp16 copy from fwav_pool_embed) selects the fp16 pre-filter
+// kernel; NULL runs the all-f32-MFMA kernel.  Both return identical candidates.
+int fwav_sim_topk(const float* emb, const void* emb16, int64_t nd, const int32_t* active, const int32_t* n_active,
+                  int64_t max_q, int64_t q_offset, int K, int32_t* cand, void* workspace, size_t ws_bytes,
+                  void* stream) {
   FWAV_CHECK_ARG(emb && active && n_active && cand && nd > 0 && max_q >= 0, FWAV_ERR_ARG, "fwav_sim_topk: bad args");
   FWAV_CHECK_ARG(K >= 1 && K <= 64, FWAV_ERR_K, "fwav_sim_topk: K=%d outside [1, 64] (use fwav_sim_topk_large)", K);
   FWAV_CHECK_ARG(nd < (int64_t)0x7fffffff, FWAV_ERR_SHAPE, "fwav_sim_topk: nd too large");
   hipStream_t st = (hipStream_t)stream;
-  return launch_topk<128>(emb, nd, active, n_active, max_q, q_offset, K, cand, st);
+  FWAV_CHECK_ARG(emb16 == nullptr || (workspace && ws_bytes >= fwav_sim_topk_workspace_size(max_q)),
+                 FWAV_ERR_WORKSPACE, "fwav_sim_topk: workspace too small");
+  return launch_topk<128>(emb, (const _Float16*)emb16, nd, active, n_active, max_q, q_offset, K, cand, st,
+                          (uint64_t*)workspace);
+}
+
+// Diagnostic ablations of the fp16 search kernel (timing only; see k_sim_topk_f16 `dbg`).
+int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t nd, const int32_t* active, const int32_t* n_active,
+                        int64_t max_q, int64_t q_offset, int K, int32_t* cand, void* workspace, int dbg,
+                        unsigned long long* stats, void* stream) {
+  FWAV_CHECK_ARG(emb && emb16 && workspace && K >= 1 && K <= 64, FWAV_ERR_ARG, "fwav_debug_sim_topk: bad args");
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_topk_stats), &stats, sizeof(stats), 0, hipMemcpyHostToDevice,
+                               (hipStream_t)stream);
+  int rc = launch_topk<128>(emb, (const _Float16*)emb16, nd, active, n_active, max_q, q_offset, K, cand,
+                            (hipStream_t)stream, (uint64_t*)workspace, dbg);
+  unsigned long long* none = nullptr;
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_topk_stats), &none, sizeof(none), 0, hipMemcpyHostToDevice,
+                               (hipStream_t)stream);
+  return rc;
 }
 
 }  // extern "C"

@@ -113,7 +113,8 @@ def _empty(n, rs, tile, step, thr, k) -> DeviceCompressed:
 
 def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh: float = 1e-4,
                     fast_mode: bool = True, s_clip: float = 16.0, shard: Optional[tuple[int, int]] = None,
-                    keep_intermediates: bool = False, events: Optional[dict] = None) -> DeviceCompressed:
+                    keep_intermediates: bool = False, events: Optional[dict] = None,
+                    search: str = "f16") -> DeviceCompressed:
     """Run the compress hot path on ``sig`` (1-D float32 tensor on a HIP device).
 
     ``shard=(lo, hi)`` restricts candidate search and the affine solve to ranges ``[lo, hi)`` (the
@@ -167,11 +168,14 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
     tab = embed_tables(rs, dev)
     pool = torch.empty(nd * rs, dtype=torch.float32, device=dev)
     emb = torch.empty(nd * 16, dtype=torch.float32, device=dev)
+    if search not in ("f16", "f32"):
+        raise ValueError("search must be 'f16' (fp16 pre-filter + exact f32 rescoring) or 'f32'")
+    emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device=dev) if search == "f16" else None
     ws_p = size_call("fwav_pool_workspace_size", n, tile_size, rs, step)
     wsp = torch.empty(max(ws_p, 16), dtype=torch.uint8, device=dev)
     _mark(events, "pool_embed")
     call("fwav_pool_embed", sig.data_ptr(), n, tile_size, rs, step, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
-         wsp.data_ptr(), ws_p, st)
+         _p(emb16), wsp.data_ptr(), ws_p, st)
     _mark(events, "pool_embed")
     m = hi - lo
     cand = torch.empty(max(m, 1) * k, dtype=torch.int32, device=dev)
@@ -189,7 +193,10 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
              emb.data_ptr(), nd, k, cand.data_ptr(), active.data_ptr(), n_active.data_ptr(), st)
         _mark(events, "prune")
         _mark(events, "sim_topk")
-        call("fwav_sim_topk", emb.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), m, lo, k, cand.data_ptr(), st)
+        wk = size_call("fwav_sim_topk_workspace_size", m) if emb16 is not None else 0
+        wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
+        call("fwav_sim_topk", emb.data_ptr(), _p(emb16), nd, active.data_ptr(), n_active.data_ptr(), m, lo, k,
+             cand.data_ptr(), wsk.data_ptr(), wk, st)
         _mark(events, "sim_topk")
         _mark(events, "affine")
         call("fwav_affine", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd,

@@ -127,3 +127,33 @@ def test_reference_e2e_tone(tmp_path):
     assert snr > 4.0
     g = load("tone")
     assert fw.read_bytes() == g["fwav_32"].tobytes() or len(matches) == len(g["m_idx_32"])
+
+
+def _cands(sig, tile, K, search, thr=1e-4):
+    r = engine.compress_device(td(sig), tile, K, energy_thresh=thr, keep_intermediates=True, search=search)
+    torch.cuda.synchronize()
+    return r.cand.cpu().numpy().reshape(-1, K), r
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_f16_prefilter_equals_f32_search(case):
+    """The fp16 pre-filter kernel must select exactly the f32 kernel's candidates (same order)."""
+    g = load(case)
+    for K in g["p"]["Ks"]:
+        if K > 64:
+            continue
+        a, ra = _cands(g["signal"], g["p"]["tile"], K, "f16")
+        b, rb = _cands(g["signal"], g["p"]["tile"], K, "f32")
+        assert np.array_equal(a, b)
+        for x, y in ((ra.idx, rb.idx), (ra.s, rb.s), (ra.o, rb.o), (ra.sym, rb.sym), (ra.err, rb.err)):
+            assert bit_equal(x.cpu().numpy(), y.cpu().numpy())
+
+
+@pytest.mark.parametrize("gen,tile,K", [("noise", 2048, 64), ("speech", 4096, 64), ("noise", 1024, 32),
+                                        ("speech", 2048, 17)])
+def test_f16_prefilter_equals_f32_larger(gen, tile, K):
+    from fwav import synth
+    sig = synth.noise(6.0, 44100, seed=11) if gen == "noise" else synth.speech_like(6.0, 44100, seed=5)
+    a, _ = _cands(sig, tile, K, "f16")
+    b, _ = _cands(sig, tile, K, "f32")
+    assert np.array_equal(a, b)

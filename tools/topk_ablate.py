@@ -1,0 +1,46 @@
+"""Time the similarity search kernel with diagnostic ablations (tools only; outputs are wrong for dbg != 0)."""
+import os, sys, time
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd")]
+import torch
+import __graft_entry__
+__graft_entry__.build()
+from fwav import engine, synth
+from fwav._lib import call
+
+secs = float(sys.argv[1]) if len(sys.argv) > 1 else 60.0
+sig = torch.from_numpy(synth.noise(secs, 44100)).cuda()
+r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
+torch.cuda.synchronize()
+nd, nr = r.n_domains, r.n_ranges
+emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+# rebuild emb16 through the pool+embed entry point
+r2 = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
+st = torch.cuda.current_stream().cuda_stream
+tab = engine.embed_tables(8, torch.device("cuda"))
+pool = torch.empty(nd * 8, device="cuda"); emb = torch.empty(nd * 16, device="cuda")
+ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
+call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
+     emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+active = torch.arange(nr, dtype=torch.int32, device="cuda")
+n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
+cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
+from fwav._lib import size_call
+wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nr), dtype=torch.uint8, device="cuda")
+stats = torch.zeros(8, dtype=torch.int64, device="cuda")
+call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
+     64, cand.data_ptr(), wsk.data_ptr(), 0, stats.data_ptr(), st)
+torch.cuda.synchronize()
+sv = stats.cpu().tolist()
+waves = (nr + 255) // 256 * 8
+print("per wave: slow_chunk calls %.1f, firing tiles %.1f, appends/query %.1f, compactions/query %.2f, "
+      "slow cycles %.3g, compaction cycles %.3g, kernel cycles %.3g" % (sv[0] / waves, sv[1] / waves, sv[2] / nr,
+      sv[3] / nr, sv[4] / waves, sv[5] / waves, sv[6] / waves), flush=True)
+for dbg in [0, 1, 3, 7, 5, 4, 2]:
+    for rep in range(2):
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
+             64, cand.data_ptr(), wsk.data_ptr(), dbg, None, st)
+        e1.record(); torch.cuda.synchronize()
+    print(f"dbg={dbg}: {e0.elapsed_time(e1):.2f} ms", flush=True)
