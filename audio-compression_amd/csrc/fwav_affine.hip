@@ -15,6 +15,7 @@
 // tie/NaN rules (first NaN wins, else smallest err, else lowest slot).
 // Bytes per range: 4·rs (range) + 4·K (candidates) + 4·K·rs (gathered rows) + 17 (outputs).
 #include "fwav_common.h"
+#include "../../include/fwav.h"
 
 namespace fwav {
 

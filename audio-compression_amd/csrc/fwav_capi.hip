@@ -2,6 +2,7 @@
 #include <cstdarg>
 
 #include "fwav_common.h"
+#include "../../include/fwav.h"
 
 namespace fwav {
 static thread_local char g_err[512] = "";

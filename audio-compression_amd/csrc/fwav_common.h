@@ -110,9 +110,11 @@ __device__ __forceinline__ float key2f(uint32_t k) {
 }  // namespace fwav
 
 // C-ABI status codes (mirrored in include/fwav.h).
+#ifndef FWAV_OK
 #define FWAV_OK 0
 #define FWAV_ERR_ARG (-1)
 #define FWAV_ERR_SHAPE (-2)
 #define FWAV_ERR_K (-3)
 #define FWAV_ERR_HIP (-4)
 #define FWAV_ERR_WORKSPACE (-5)
+#endif

@@ -16,6 +16,7 @@
 // decision can differ, and only when Δ lies within rounding of eps.
 // Bytes per range per iteration: 4·rs (rec) + 4·rs (next) + 4·rs (T) + 16 (mean, den, s, o) + 1 (valid).
 #include "fwav_common.h"
+#include "../../include/fwav.h"
 
 namespace fwav {
 

@@ -17,6 +17,7 @@
 //   transient[k] = Σ_n C[k][n]·w[n]·f64(x[n] − x[n−1]),  k < min(8, rs); f64 norm; /‖·‖ if > 1e-8; → f32
 // Parity is |Δ| ≤ 1e-6 against the reference goldens (SURVEY Appendix A rule 2).
 #include "fwav_common.h"
+#include "../../include/fwav.h"
 
 namespace fwav {
 

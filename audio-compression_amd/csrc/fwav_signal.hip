@@ -10,6 +10,7 @@
 //   k_voiced_decide (per frame, + per-block last decisive position) → k_voiced_carry (one block, exclusive
 //   prefix max over blocks) → k_frame_state (in-block max-scan + carry) → k_form_ranges (per sample).
 #include "fwav_common.h"
+#include "../../include/fwav.h"
 
 namespace fwav {
 

@@ -22,6 +22,7 @@
 //     later domain whose score equals θ can never displace an earlier one: strict '>' is exact.
 // The chunk for the next iteration is prefetched into registers while the current one is consumed.
 #include "fwav_common.h"
+#include "../../include/fwav.h"
 
 namespace fwav {
 

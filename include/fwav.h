@@ -1,0 +1,117 @@
+/* fwav.h — C ABI of libfwav.so, the MI355X (gfx950) hot path of the fractal WAV codec.
+ *
+ * Drop-in boundary for xavenordu/Audio-Compression (reference: /root/reference/fractal.py).  The reference is
+ * pure Python; its hot path is the xp (NumPy/CuPy) code inside compress_audio / decompress_audio.  Each entry
+ * point below replaces one of those stages and cites the lines it replaces.  The Python host
+ * (audio-compression_amd/fwav) binds these with ctypes; INTEGRATION.md shows that binding.
+ *
+ * Conventions
+ *   - All array pointers are DEVICE pointers (HBM) owned by the caller; sizes are element counts.
+ *   - `stream` is a hipStream_t passed as void*; every call only enqueues work on it (no host sync, no
+ *     allocation) unless stated otherwise, so a caller may capture the sequence in a hipGraph.
+ *   - Return value: 0 = FWAV_OK, negative = error; fwav_last_error() returns a thread-local message.
+ *     No exception, abort or exit crosses the ABI.
+ *   - Workspaces are caller-allocated; *_workspace_size() gives the byte count.
+ *   - Results are deterministic for identical inputs.
+ */
+#ifndef FWAV_H
+#define FWAV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FWAV_OK 0
+#define FWAV_ERR_ARG (-1)       /* null pointer / invalid argument */
+#define FWAV_ERR_SHAPE (-2)     /* sizes inconsistent or outside supported range */
+#define FWAV_ERR_K (-3)         /* top-K outside the supported range */
+#define FWAV_ERR_HIP (-4)       /* HIP runtime / launch error */
+#define FWAV_ERR_WORKSPACE (-5) /* workspace missing or too small */
+
+/* ---------------------------------------------------------------------------------------- plumbing */
+const char* fwav_last_error(void);
+int fwav_abi_version(void);
+/* Blocks until `stream` is idle; surfaces asynchronous kernel faults as FWAV_ERR_HIP. */
+int fwav_stream_sync(void* stream);
+
+/* ------------------------------------------------------------- voiced detection + range formation
+ * Replaces voiced_detection (fractal.py:880-909) and the range setup of compress_audio
+ * (fractal.py:1074-1112): frame energies (frame = 2·range_size, reflect-padded, numpy pairwise mean),
+ * `smooth_window`-tap moving average (np.convolve 'same' order), hysteresis hi/lo (float32 compares),
+ * ranges[p] = (signal·mask)[reflect(p)] for p < n_ranges·range_size, n_ranges = ceil(n / range_size).
+ * hi = float32(energy_thresh), lo = float32(0.5·energy_thresh).  mask_out (u8[n]) may be NULL. */
+size_t fwav_voiced_workspace_size(int64_t n, int frame);
+int fwav_voiced_ranges(const float* sig, int64_t n, int range_size, int frame, int smooth_window, float hi, float lo,
+                       float* ranges, int64_t n_ranges, uint8_t* mask_out, void* workspace, size_t ws_bytes,
+                       void* stream);
+
+/* Silent-input test of compress_audio (fractal.py:1083): per-block f64 partial sums of ranges[0:n]² into
+ * partial[nblocks]; the caller adds them (f64) and compares with 1e-8. */
+int fwav_weighted_energy(const float* ranges, int64_t n, double* partial, int nblocks, void* stream);
+
+/* ------------------------------------------------------------------- domain pool + embeddings
+ * Replaces build_domains_memmap (fractal.py:285-334) and build_domain_embeddings → multi_head_embedding →
+ * tile_embedding / transient_embedding (fractal.py:238-280, 166-208, 154-164).
+ * pool f32[n_domains·range_size] (bit-exact), emb f32[n_domains·16] (|Δ| ≤ 1e-6 vs the reference),
+ * emb16 (optional) fp16 copy in the similarity search's tiled layout, f16[ceil(n_domains/256)·256·16].
+ * n_domains = (n − tile) / step + 1.  tab = device copy of fwav_embed_tables(range_size) (host call). */
+int fwav_embed_tables(int range_size, double* tab_host /* [16·range_size] */);
+size_t fwav_pool_workspace_size(int64_t n, int tile, int range_size, int step);
+int fwav_pool_embed(const float* sig, int64_t n, int tile, int range_size, int step, const double* tab, float* pool,
+                    float* emb, void* emb16, void* workspace, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------- energy prune + degenerate queries
+ * Replaces the per-range prefix of cpu_worker (fractal.py:598-622) for ranges [q_offset, q_offset + n):
+ *   mean(r²) < prune_thr (= float32(0.75·energy_thresh), fast_mode) → cand row all −1;
+ *   query embedding (domain row q_offset + i, quirk Q1 fractal.py:1190-1195) all zero → cand row 0..K−1;
+ *   otherwise local index i is appended to active[] (*n_active, device counter) for fwav_sim_topk. */
+int fwav_prune(const float* ranges, int64_t n, int64_t q_offset, int range_size, float prune_thr, int fast_mode,
+               const float* emb, int64_t n_domains, int k, int32_t* cand, int32_t* active, int32_t* n_active,
+               void* stream);
+
+/* ------------------------------------------------------------------- similarity top-K
+ * Replaces range_candidates_from_embedding_emb + pad_candidates (fractal.py:535-552, 617-622): for each
+ * local query listed in active[0 .. *n_active) (at most max_q), the K domains with the largest f32 score
+ * fma_k(emb[d][k]·emb[q_offset+i][k]) in (score desc, index asc) order, −1-padded when n_domains < K,
+ * into cand[i·K .. i·K+K).  emb16 != NULL selects the fp16 MFMA pre-filter + exact f32 rescoring kernel
+ * (needs `workspace` of fwav_sim_topk_workspace_size(max_q) bytes); emb16 == NULL runs the all-f32 MFMA
+ * kernel.  Both return identical candidates.  1 ≤ K ≤ fwav_topk_max_k(). */
+int fwav_topk_max_k(void);
+size_t fwav_sim_topk_workspace_size(int64_t max_q);
+int fwav_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
+                  const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand, void* workspace,
+                  size_t ws_bytes, void* stream);
+/* Diagnostic ablations of the fp16 kernel (timing only, outputs invalid for dbg != 0); stats (u64[8] device,
+ * may be NULL) receives slow-path counters.  Not used by the product path. */
+int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
+                        const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand,
+                        void* workspace, int dbg, unsigned long long* stats, void* stream);
+
+/* ------------------------------------------------------------------- batched affine solve
+ * Replaces _flush_gpu_batch / _process_gpu_batch (fractal.py:852-870, 757-850): per range, over the K
+ * candidates and their mirrors, s = Σd̃r̃/(Σd̃²+1e-12), o = r̄ − s·d̄, err = ‖s·D+o−R‖₂ (+inf for cand < 0),
+ * first minimum over [K | K mirrored]; outputs (cand clamped to ≥ 0, clip(s, ±s_clip), o, sym, err),
+ * bit-exact with the reference's float32 numpy arithmetic. */
+int fwav_affine(const float* ranges, int64_t n_ranges, int range_size, const int32_t* cand, int k, const float* pool,
+                int64_t n_domains, float s_clip, int32_t* out_idx, float* out_s, float* out_o, uint8_t* out_sym,
+                float* out_err, void* stream);
+
+/* ------------------------------------------------------------------- decompression loop
+ * Replaces decompress_audio (fractal.py:1378-1473): all `iterations` launches are queued at once; a device
+ * flag stops the work once Δ = ‖next − rec‖/(‖rec‖ or 1) < eps (Δ in f64).  state[0] = converged flag,
+ * state[1] = iterations run (t); result in recon_b if t is odd, else recon_a; deltas[0..t) = Δ per
+ * iteration.  recon values are bit-exact with the reference. */
+size_t fwav_decode_workspace_size(int64_t n_ranges, int range_size, int iterations);
+int fwav_decode(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t n_ranges,
+                int range_size, const float* pool, int64_t n_domains, int iterations, double eps, float s_clip,
+                double s_damping, float* recon_a, float* recon_b, double* deltas, int* state, void* workspace,
+                size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FWAV_H */

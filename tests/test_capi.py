@@ -1,0 +1,82 @@
+"""The C-ABI library: loads on CPU, exports exactly what include/fwav.h declares, binds with the right arity,
+rejects bad arguments with status codes (no GPU needed: argument checks run before any HIP call)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fwav.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*(?:const\s+)?[\w]+\s*\*?\s*(fwav_\w+)\s*\(([^;]*?)\);", txt, flags=re.M | re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import __graft_entry__
+    __graft_entry__.build()
+    from fwav import _lib
+    return _lib
+
+
+def test_header_symbols_exported(lib):
+    decl = header_functions()
+    assert len(decl) >= 15
+    dll = ctypes.CDLL(lib.LIB_PATH)
+    for name in decl:
+        assert hasattr(dll, name), f"{name} declared in include/fwav.h but not exported"
+
+
+def test_bindings_match_header(lib):
+    decl = header_functions()
+    assert set(decl) == set(lib.SIGNATURES), set(decl) ^ set(lib.SIGNATURES)
+    for name, n in decl.items():
+        assert len(lib.SIGNATURES[name][1]) == n, name
+
+
+def test_error_codes_without_gpu(lib):
+    L = lib.lib()
+    assert L.fwav_abi_version() == 1
+    rc = L.fwav_affine(None, 10, 8, None, 64, None, 100, 16.0, None, None, None, None, None, None)
+    assert rc == -1 and b"null" in L.fwav_last_error()
+    rc = L.fwav_sim_topk(None, None, 10, None, None, 10, 0, 64, None, None, 0, None)
+    assert rc == -1
+    big = ctypes.c_void_p(16)
+    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 4096, big, None, 0, None)
+    assert rc == -3 and b"K=" in L.fwav_last_error()
+
+
+def test_embed_tables_match_scipy_dct(lib):
+    """fwav_embed_tables is a host function: its rows are the ortho DCT-II rows × linspace weights."""
+    import scipy.fftpack
+    L = lib.lib()
+    for rs in (4, 8, 16, 13):
+        tab = np.zeros(16 * rs)
+        assert L.fwav_embed_tables(rs, tab.ctypes.data) == 0
+        eye = np.eye(rs)
+        D = scipy.fftpack.dct(eye, norm="ortho", axis=0)  # D[k, n]
+        w = np.linspace(1.0, 2.0, rs)
+        take, tk = min(8, rs - 1), min(8, rs)
+        ton = tab[:8 * rs].reshape(8, rs)
+        tra = tab[8 * rs:].reshape(8, rs)
+        np.testing.assert_allclose(ton[:take], D[1:1 + take] * w[1:1 + take, None], atol=1e-14)
+        np.testing.assert_allclose(tra[:tk], D[:tk] * w[None, :], atol=1e-14)
+        assert np.all(ton[take:] == 0) and np.all(tra[tk:] == 0)
+
+
+def test_workspace_sizes(lib):
+    from fwav._lib import size_call
+    assert size_call("fwav_voiced_workspace_size", 2646000, 16) > 0
+    assert size_call("fwav_pool_workspace_size", 2646000, 2048, 8, 2) == ((2646000 - 2048) // 2 + 1 + 7 * 128) * 4
+    assert size_call("fwav_pool_workspace_size", 1000, 2048, 8, 2) == 0
+    assert size_call("fwav_sim_topk_workspace_size", 330750) >= 330750 * 64 * 8

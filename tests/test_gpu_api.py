@@ -1,0 +1,71 @@
+"""GPU: the fractal-compatible API surface — reference edge cases, sentinels, shards, CLI end to end."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN, bit_equal
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def test_reference_edge_cases():
+    import fractal
+    from fwav import synth
+    edges = json.load(open(os.path.join(GOLDEN, "edges.json")))
+    r = fractal.compress_audio(synth.noise(0.01, 44100, seed=5), 44100, 4, tile_size=2048)
+    assert len(r[0]) == edges["short"]["n_matches"] and list(r[1].shape) == edges["short"]["pool_shape"]
+    assert [int(r[2]), int(r[3]), int(r[4]), int(r[5]), float(r[6]), int(r[7])] == edges["short"]["rest"]
+    r = fractal.compress_audio(np.zeros(5000, np.float32), 44100, 4, tile_size=1024)
+    assert len(r[0]) == 0 and list(r[1].shape) == edges["silent"]["pool_shape"]
+    assert [int(r[2]), int(r[3]), int(r[4]), int(r[5]), float(r[6]), int(r[7])] == edges["silent"]["rest"]
+    with pytest.raises(ValueError, match=edges["q9"]["msg"]):
+        fractal.compress_audio(synth.noise(1.0, 44100)[:2448], 44100, 4, tile_size=2048)
+
+
+def test_decode_sentinels_match_oracle():
+    from fwav.api import decompress_audio
+    from oracle import fractal_oracle as O
+    rng = np.random.default_rng(4)
+    nd, rs, nr = 300, 8, 200
+    pool = rng.normal(size=(nd, rs)).astype(np.float32)
+    pool[7] = 1.0  # constant tile: denominator 0 → stored s used
+    idx = rng.integers(-1, nd, nr).astype(np.int32)
+    idx[::17] = 7
+    s = rng.normal(size=nr).astype(np.float32) * 3
+    o = rng.normal(size=nr).astype(np.float32)
+    sym = rng.integers(0, 2, nr).astype(np.uint8)
+    m = list(zip(idx.tolist(), s.tolist(), o.tolist(), sym.tolist(), [0.0] * nr))
+    for kw in (dict(), dict(iterations=20, convergence_eps=0.0), dict(iterations=9, convergence_eps=0.0, s_damping=0.5),
+               dict(iterations=5, s_clip=0.75)):
+        d, info = decompress_audio(m, pool, nr, rs, original_len=nr * rs - 3, return_info=True, **kw)
+        ref, it, _ = O.decode(idx, s, o, sym, pool, nr, rs, original_len=nr * rs - 3, **kw)
+        assert bit_equal(d, ref) and info["iterations"] == it
+
+
+def test_shards_concatenate_to_full_run():
+    from fwav import engine, synth
+    sig = torch.from_numpy(synth.speech_like(3.0, 44100, seed=9, floor=False)).cuda()
+    full = engine.compress_device(sig, 2048, 32, keep_intermediates=True)
+    nr = full.n_ranges
+    cuts = [0, 1000, 1001, 4000, nr]
+    parts = [engine.compress_device(sig, 2048, 32, shard=(a, b)) for a, b in zip(cuts[:-1], cuts[1:])]
+    torch.cuda.synchronize()
+    for f in ("idx", "s", "o", "sym", "err"):
+        cat = np.concatenate([getattr(p, f).cpu().numpy() for p in parts])
+        assert bit_equal(cat, getattr(full, f).cpu().numpy()), f
+
+
+def test_cli_roundtrip(tmp_path):
+    from fwav import synth
+    from fwav.cli import main
+    from fwav.fwavio import write_wav
+    wav = tmp_path / "a.wav"
+    write_wav(str(wav), synth.noise(0.5, 22050, seed=3), 22050, 4)
+    out = tmp_path / "out"
+    r = main(["compress", str(wav), str(out), "--tile", "1024"])
+    assert "error" not in r and os.path.exists(out / "a.wav.fwav")
+    r = main(["decompress", str(out / "a.wav.fwav"), "--out", str(tmp_path / "rec")])
+    assert "error" not in r and os.path.exists(tmp_path / "rec" / "a.wav.fwav_recon.wav")

@@ -1,0 +1,85 @@
+"""Pin the oracle (CPU restatement) against the reference's own outputs (tests/golden, made by
+tests/golden/make_golden.py from /root/reference/fractal.py).  Bars: SURVEY.md Appendix A."""
+import numpy as np
+import pytest
+
+from golden_util import CASES, bit_equal, candidate_agreement, load
+from oracle import fractal_oracle as O
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_voiced_ranges_pool_bitexact(case):
+    g = load(case)
+    p = g["p"]
+    rs, step = O.geometry(p["tile"])
+    assert (rs, step) == (p["rs"], p["step"])
+    vm = O.voiced_detection(g["signal"], 2 * rs, p["thr"])
+    assert np.array_equal(vm, g["voiced"])
+    r, orig = O.form_ranges(g["signal"], vm, rs)
+    assert orig == p["original_len"]
+    assert bit_equal(r, g["ranges"])
+    assert bit_equal(O.domain_pool(g["signal"], p["tile"], rs, step), g["pool"])
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_embedding_tolerance(case):
+    g = load(case)
+    emb = O.embed(g["pool"])
+    assert np.abs(emb - g["emb"]).max() <= 1e-6
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_candidates_near_tie_rule(case):
+    g = load(case)
+    p = g["p"]
+    pruned = O.range_energy_pruned(g["ranges"], p["thr"])
+    for K in p["Ks"]:
+        gold = g[f"cand_{K}"]
+        assert np.array_equal(pruned, gold[:, 0] < 0)
+        cand, _, _ = O.topk_candidates(g["emb"], len(gold), K, pruned)
+        _, bad = candidate_agreement(cand, gold, g[f"kth_{K}"], g[f"k1th_{K}"], g["emb"][:len(gold)], pruned)
+        assert not bad.any()
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_affine_bitexact(case):
+    g = load(case)
+    for K in g["p"]["Ks"]:
+        out = O.affine(g["ranges"], g[f"cand_{K}"], g["pool"])
+        for nm, a in zip(("idx", "s", "o", "sym", "err"), out):
+            assert bit_equal(a, g[f"m_{nm}_{K}"]), nm
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_decode_bitexact(case):
+    g = load(case)
+    p = g["p"]
+    for K in p["Ks"]:
+        args = (g[f"m_idx_{K}"], g[f"m_s_{K}"], g[f"m_o_{K}"], g[f"m_sym_{K}"], g["pool"], len(g[f"m_idx_{K}"]),
+                p["rs"])
+        d, it, _ = O.decode(*args, original_len=p["original_len"])
+        assert bit_equal(d, g[f"dec_{K}"]) and it == int(g[f"dec_iters_{K}"])
+        d, _, _ = O.decode(*args, iterations=50, convergence_eps=0.0, original_len=p["original_len"])
+        assert bit_equal(d, g[f"dec50_{K}"])
+        d, it, dl = O.decode(*args, iterations=12, convergence_eps=0.0, s_damping=0.3, original_len=p["original_len"])
+        assert bit_equal(d, g[f"decd_{K}"])
+        np.testing.assert_allclose(dl, g[f"decd_deltas_{K}"], rtol=1e-5)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c in ("tone", "sweep", "ragged")])
+def test_fwav_bytes(case):
+    g = load(case)
+    p = g["p"]
+    for K in p["Ks"]:
+        b = O.fwav_bytes(g[f"m_idx_{K}"], g[f"m_s_{K}"], g[f"m_o_{K}"], g[f"m_sym_{K}"], g[f"m_err_{K}"], g["pool"],
+                         p["rs"], p["framerate"], p["sampwidth"], p["tile"], p["step"], p["thr"], p["original_len"])
+        assert b == g[f"fwav_{K}"].tobytes()
+
+
+def test_pruned_ranges_emit_domain0_inf():
+    """Quirk Q3: all-(-1) candidates → domain 0 (clamped) with s/o fitted to domain 0 and err=+inf."""
+    g = load("speech4096")
+    K = 64
+    pr = g[f"cand_{K}"][:, 0] < 0
+    assert pr.any()
+    assert np.all(g[f"m_idx_{K}"][pr] == 0) and np.all(np.isinf(g[f"m_err_{K}"][pr]))
