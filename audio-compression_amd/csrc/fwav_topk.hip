@@ -244,16 +244,21 @@ constexpr float kF16Delta = 2.5e-3f;
 
 // Diagnostic counters (fwav_debug_sim_topk only; stays nullptr in production launches):
 //   [0] slow_chunk calls  [1] firing tiles  [2] appends  [3] compactions
-//   [4] cycles in slow_chunk  [5] cycles in compactions  [6] cycles per wave (whole kernel)
-__device__ unsigned long long* g_topk_stats = nullptr;
-__device__ __forceinline__ void stat_add(int i, unsigned long long v) {
-  if (g_topk_stats != nullptr && (threadIdx.x & 63) == 0) atomicAdd(g_topk_stats + i, v);
+//   [4] ticks in slow_chunk  [5] ticks in compactions  [6] ticks per wave (whole kernel)
+//   [7] ticks draining stores  [8] ticks loading keys+rows  [9] ticks sorting   (s_memrealtime, 100 MHz)
+#define g_topk_stats stats
+__device__ __forceinline__ void stat_add_p(unsigned long long* stats, int i, unsigned long long v) {
+  if (stats != nullptr && (threadIdx.x & 63) == 0) atomicAdd(stats + i, v);
 }
+#define stat_add(i, v) stat_add_p(stats, (i), (v))
 constexpr int kGroup = 4;            // chunks per barrier (and per register prefetch group)
 constexpr int k16Waves = 8;
 constexpr int k16Q = 32 * k16Waves;  // queries per workgroup
 constexpr int k16Threads = 64 * k16Waves;
 constexpr int k16Cap = 256;          // key-buffer entries per query (global workspace)
+constexpr int kWindowGroups = 8;     // after the warm-up, deferred slow work is replayed every 8 groups
+constexpr int kWarmChunks = 64;      // ... and after every group during the first 64 chunks
+
 
 __device__ __forceinline__ float score32(const float* __restrict__ emb, int64_t d, const float (&q)[16]) {
   const float4* p = reinterpret_cast<const float4*>(emb + d * 16);
@@ -291,10 +296,71 @@ __device__ __forceinline__ bool may_pass(int imx, float thf) {
 
 struct Topk16Smem {
   int cnt[k16Q];      // entries in the query's buffer
-  int nex[k16Q];      // leading entries that are exact (sorted top-K after the last compaction)
-  float theta[k16Q];  // exact K-th score (−inf until K entries)
+  int nex[k16Q];      // final pass: leading entries that are exact
+  float theta[k16Q];  // filter threshold on s16 (append iff s16 > theta)
+  int ovf[k16Q];      // band overflowed the buffer: recompute this query with the f32 kernel
   int64_t qrow[k16Q];
+  uint32_t fired[k16Waves][kWindowGroups * kGroup];  // per-wave deferred work: chunk indices of a window
 };
+
+// Streaming compaction on fp16-MFMA keys (no f32 rescoring, no table loads): sort the buffer by s16,
+// S16 = K-th largest; every exact top-K member has s16 > S16 − 2δ (K domains have s32 > S16 − δ), so keep
+// exactly that band and filter new domains with it.  If the band would not leave 64 free slots the query
+// is flagged (ovf) and later recomputed by the exact f32 kernel.
+template <int C>
+__device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, Topk16Smem& sm, int ql, int K,
+                                              unsigned long long* stats) {
+  constexpr int E = C / 64;
+  const unsigned long long t_start = stats ? __builtin_amdgcn_s_memrealtime() : 0;
+  const int lane = threadIdx.x & 63;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t_drained = stats ? __builtin_amdgcn_s_memrealtime() : 0;
+  const int n = sm.cnt[ql];
+  uint64_t v[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    v[j] = e < n ? kq[e] : 0ull;
+  }
+  const unsigned long long t_loaded = stats ? __builtin_amdgcn_s_memrealtime() : 0;
+  wave_sort_desc<E>(v);
+  const unsigned long long t_sorted = stats ? __builtin_amdgcn_s_memrealtime() : 0;
+  int m = n;
+  float lim = -INFINITY;
+  if (n >= K) {
+    const int kl = (K - 1) & 63, kj = (K - 1) >> 6;
+    uint64_t kth = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (j == kj) kth = __shfl(v[j], kl);
+    lim = key_score(kth) - 2.0f * kF16Delta;
+    m = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) m += __popcll(__ballot(j * 64 + lane < n && key_score(v[j]) > lim));
+  }
+  int ovf = 0;
+  if (m > C - 64) {
+    m = C - 64;
+    ovf = 1;
+  }
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    if (e < m) kq[e] = v[j];
+  }
+  if (lane == 0) {
+    sm.cnt[ql] = m;
+    sm.theta[ql] = lim;
+    if (ovf) sm.ovf[ql] = 1;
+  }
+  if (stats) {
+    stat_add(3, 1);
+    stat_add(5, __builtin_amdgcn_s_memrealtime() - t_start);
+    stat_add(7, t_drained - t_start);
+    stat_add(8, t_loaded - t_drained);
+    stat_add(9, t_sorted - t_loaded);
+  }
+}
 
 // Rescore the inexact tail of query ql's buffer kq[0..C), sort, keep the top K, set θ.  Whole wave.
 // Every per-query buffer and counter is owned by one wave, so no cross-wave fences are needed; the wave's
@@ -302,11 +368,12 @@ struct Topk16Smem {
 // together (two memory round trips in total).
 template <int C>
 __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, Topk16Smem& sm, int ql, int K,
-                                          const float* __restrict__ emb) {
+                                          const float* __restrict__ emb, unsigned long long* stats) {
   constexpr int E = C / 64;
-  const unsigned long long t_start = g_topk_stats ? __builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long t_start = g_topk_stats ? __builtin_amdgcn_s_memrealtime() : 0;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t_drained = g_topk_stats ? __builtin_amdgcn_s_memrealtime() : 0;
   const int n = sm.cnt[ql];
   const int ne = sm.nex[ql];
   const float4* qp = reinterpret_cast<const float4*>(emb + sm.qrow[ql] * 16);
@@ -331,7 +398,7 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, Topk16Smem&
     for (int jj = 0; jj < 2; ++jj) {
       const int j = j0 + jj;
       const int e = j * 64 + lane;
-      dd[jj] = (j < E && e >= ne && e < n) ? (int32_t)(uint32_t)v[j < E ? j : 0] : 0;
+      dd[jj] = (j < E && e >= ne && e < n) ? key_idx(v[j < E ? j : 0]) : 0;
       const float4* p = reinterpret_cast<const float4*>(emb + (int64_t)dd[jj] * 16);
 #pragma unroll
       for (int i = 0; i < 4; ++i) row[jj][i] = p[i];
@@ -353,7 +420,14 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, Topk16Smem&
       }
     }
   }
+  const unsigned long long t_loaded = g_topk_stats ? __builtin_amdgcn_s_memrealtime() : 0;
   wave_sort_desc<E>(v);
+  if (g_topk_stats) {
+    const unsigned long long t_sorted = __builtin_amdgcn_s_memrealtime();
+    stat_add(7, t_drained - t_start);
+    stat_add(8, t_loaded - t_drained);
+    stat_add(9, t_sorted - t_loaded);
+  }
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
@@ -372,63 +446,127 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, Topk16Smem&
   }
   if (g_topk_stats) {
     stat_add(3, 1);
-    stat_add(5, __builtin_amdgcn_s_memtime() - t_start);
+    stat_add(5, __builtin_amdgcn_s_memrealtime() - t_start);
   }
 }
 
-// Slow path for one chunk (inline; taken when some lane's tile max clears θ − δ): recompute each tile's
-// MFMA from the LDS slot, append the survivors' indices to the wave-owned global key buffers (one LDS
-// atomic per lane per tile reserves the slot range), compact full buffers.  Returns the new θ − δ.
-template <int C>
-__device__ __forceinline__ float slow_chunk(const _Float16* __restrict__ lda, half8 b, float thf, int64_t dbase,
-                                            int64_t nd, uint64_t* __restrict__ gkeys, Topk16Smem& sm, int K,
-                                            const float* __restrict__ emb, int upd) {
+// Integer filter threshold for the fold-max test: (int)x > thi ⟺ x > thf for non-NaN x when thf >= 0;
+// for thf < 0 every tile goes to the exact per-score test.
+__device__ __forceinline__ int int_threshold(float thf) {
+  return thf < 0.0f ? (int)0x80000000 : __float_as_int(thf);
+}
+
+__device__ __forceinline__ int fold16(int r, const floatx16& a) {
+  auto I = [&](int i) { return __float_as_int(a[i]); };
+  auto m3 = [](int x, int y, int z) { return max(max(x, y), z); };
+  r = m3(r, I(0), I(1));
+  r = m3(r, I(2), I(3));
+  r = m3(r, I(4), I(5));
+  r = m3(r, I(6), I(7));
+  r = m3(r, I(8), I(9));
+  r = m3(r, I(10), I(11));
+  r = m3(r, I(12), I(13));
+  return m3(r, I(14), I(15));
+}
+
+// Fired chunk (rare after the warm-up): recompute each tile's MFMA from the still-valid LDS slot, append
+// the survivors (s16 keys) to the wave-owned global key buffers — one LDS atomic per lane per tile
+// reserves the slots; the stores are fire-and-forget — and compact a buffer inline only when it is about
+// to overflow (hard limit).  Ordinary compactions wait for the window end (compact_pending).
+template <int C, bool STATS>
+__device__ __forceinline__ float append_tiles(const half8 (&af)[8], half8 b, float thf, int64_t dbase,
+                                              int64_t nd, uint64_t* __restrict__ gkeys, Topk16Smem& sm, int K,
+                                              int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int col = lane & 31;
   const int h = lane >> 5;
   const int ql = wave * 32 + col;
   uint64_t* kq = gkeys + (size_t)ql * C;
-  stat_add(0, 1);
+  if (STATS) stat_add(0, 1);
+  const bool last = dbase + kChunk > nd;
+#pragma unroll
   for (int t = 0; t < 8; ++t) {
-    const half8 a = *reinterpret_cast<const half8*>(lda + ((h * kChunk) + t * 32 + col) * 8);
-    const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, floatx16{}, 0, 0, 0);
+    const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[t], b, floatx16{}, 0, 0, 0);
+    if (__ballot(fold16((int)0x80000000, acc) > int_threshold(thf)) == 0ull) continue;
+    if (STATS) stat_add(1, 1);
     const int64_t d0 = dbase + t * 32 + 4 * h;
     uint32_t mask = 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t d = d0 + (r & 3) + 8 * (r >> 2);
-      mask |= (acc[r] > thf && d < nd) ? (1u << r) : 0u;
+    for (int r = 0; r < 16; ++r) mask |= acc[r] > thf ? (1u << r) : 0u;
+    if (last) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (d0 + (r & 3) + 8 * (r >> 2) >= nd) mask &= ~(1u << r);
     }
-    if (__ballot(mask != 0u) == 0ull) continue;
-    stat_add(1, 1);
     const int cntm = __builtin_popcount(mask);
-    int base = 0;
-    if (cntm) base = atomicAdd(&sm.cnt[ql], cntm);
+    int base_i = 0;
+    if (cntm) base_i = atomicAdd(&sm.cnt[ql], cntm);
     while (mask) {
       const int r = __builtin_ctz(mask);
       mask &= mask - 1;
-      kq[base++] = (uint64_t)(uint32_t)(d0 + (r & 3) + 8 * (r >> 2));
+      kq[base_i++] = make_key(acc[r], (int32_t)(d0 + (r & 3) + 8 * (r >> 2)));
     }
-    if (g_topk_stats && cntm) atomicAdd(g_topk_stats + 2, (unsigned long long)cntm);
+    if (STATS && cntm) atomicAdd(stats + 2, (unsigned long long)cntm);
     uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > C - 32);
     while (need != 0ull) {
       const int l = __builtin_ctzll(need);
       need &= need - 1;
-      compact16<C>(gkeys + (size_t)(wave * 32 + l) * C, sm, wave * 32 + l, K, emb);
+      compact16_s16<C>(gkeys + (size_t)(wave * 32 + l) * C, sm, wave * 32 + l, K, STATS ? stats : nullptr);
     }
-    if (upd) thf = sm.theta[ql] - kF16Delta;
+    if (upd) thf = sm.theta[ql];
   }
   return thf;
 }
 
-template <int C>
+// Window end: replay the chunks this wave recorded as fired.  Each chunk's 8 fragments are re-read from the
+// fp16 table (L2-resident: streamed at most one window ago) in one batch, then append_tiles runs on them.
+template <int C, bool STATS>
+__device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int nf,
+                                               int64_t nd, uint64_t* __restrict__ gkeys, Topk16Smem& sm, int K,
+                                               int upd, unsigned long long* stats) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int col = lane & 31;
+  const int h = lane >> 5;
+  for (int f = 0; f < nf; ++f) {
+    const int64_t c = sm.fired[wave][f];
+    const _Float16* base = emb16 + ((c * 2 + h) * kChunk + col) * 8;
+    half8 af[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) af[t] = *reinterpret_cast<const half8*>(base + t * 256);
+    thf = append_tiles<C, STATS>(af, b, thf, c * kChunk, nd, gkeys, sm, K, upd, stats);
+  }
+  return thf;
+}
+
+// Window end: compact every buffer of this wave that passed the soft limit.
+template <int C, bool STATS>
+__device__ __forceinline__ float compact_pending(float thf, uint64_t* __restrict__ gkeys, Topk16Smem& sm, int K,
+                                                 int upd, unsigned long long* stats) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int ql = wave * 32 + (lane & 31);
+  uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > C / 2);
+  if (need == 0ull) return thf;
+  while (need != 0ull) {
+    const int l = __builtin_ctzll(need);
+    need &= need - 1;
+    compact16_s16<C>(gkeys + (size_t)(wave * 32 + l) * C, sm, wave * 32 + l, K, STATS ? stats : nullptr);
+  }
+  return upd ? sm.theta[ql] : thf;
+}
+
+template <int C, bool STATS>
 __global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
                                                                 const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
                                                                 const int32_t* __restrict__ n_active_p,
                                                                 int64_t q_offset, int K, int32_t* __restrict__ cand,
-                                                                uint64_t* __restrict__ gkeys_all, int dbg) {
+                                                                uint64_t* __restrict__ gkeys_all,
+                                                                int32_t* __restrict__ ovf_list,
+                                                                int32_t* __restrict__ n_ovf, int dbg,
+                                                                unsigned long long* stats) {
   // 2 × kGroup chunk slots: a group of kGroup chunks is written, one barrier, then consumed; the next
   // group goes to the other half, so waves may drift up to a group apart between barriers.
   __shared__ __attribute__((aligned(16))) uint4 slots[2 * kGroup][512];
@@ -438,7 +576,7 @@ __global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* 
   const int qbase = blockIdx.x * k16Q;
   if (qbase >= n_active) return;
   uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * k16Q * C;
-  const unsigned long long t_kernel = g_topk_stats ? __builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long t_kernel = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -450,14 +588,16 @@ __global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* 
   const int32_t q = qi < n_active ? active[qi] : -1;
   const int64_t qrow = (int64_t)(q < 0 ? 0 : q) + q_offset;
   const half8 b = *reinterpret_cast<const half8*>(emb16 + (((qrow >> 8) * 2 + h) * 256 + (qrow & 255)) * 8);
-  // dbg (diagnostic ablations, timing only — outputs are wrong when set):
-  //   1 = never take the slow path, 2 = skip MFMA + threshold test, 4 = no global chunk loads
+  // dbg (STATS builds only; timing ablations, outputs invalid): 1 = never take the slow path,
+  // 2 = skip MFMA + threshold test, 4 = no global chunk loads
+  if (!STATS) dbg = 0;
   const int upd = (q >= 0 && !(dbg & 1)) ? 1 : 0;
   float thf = upd ? -INFINITY : INFINITY;
   if (h == 0) {
     sm.cnt[ql] = 0;
     sm.nex[ql] = 0;
     sm.theta[ql] = -INFINITY;
+    sm.ovf[ql] = 0;
     sm.qrow[ql] = qrow;
   }
 
@@ -474,26 +614,41 @@ __global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* 
   };
   load_group(0);
 
+  int nfired = 0;  // wave-uniform count of chunks recorded in sm.fired[wave] this window
   for (int64_t g = 0; g < ngroups; ++g) {
     uint4(*half)[512] = slots + (g & 1) * kGroup;
 #pragma unroll
     for (int j = 0; j < kGroup; ++j) half[j][tid] = pf[j];
     if (g + 1 < ngroups) load_group(g + 1);
     __syncthreads();
-    if (dbg & 2) continue;
+    if (STATS && (dbg & 2)) continue;
     const int64_t c_end = (g + 1) * kGroup < nchunks ? (g + 1) * kGroup : nchunks;
+    int thi = int_threshold(thf);
     for (int64_t c = g * kGroup; c < c_end; ++c) {
-      const _Float16* lda = reinterpret_cast<const _Float16*>(half[c - g * kGroup]);
-      int m[8];
+      const _Float16* lda = reinterpret_cast<const _Float16*>(half[c - g * kGroup]) + ((h * kChunk) + col) * 8;
+      // two tiles in flight per wave; every tile folds into one of two running max chains
+      int r0 = (int)0x80000000, r1 = (int)0x80000000;
+      half8 a0 = *reinterpret_cast<const half8*>(lda + 0 * 256);
+      half8 a1 = *reinterpret_cast<const half8*>(lda + 1 * 256);
+      floatx16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b, floatx16{}, 0, 0, 0);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const half8 a = *reinterpret_cast<const half8*>(lda + ((h * kChunk) + t * 32 + col) * 8);
-        m[t] = imax16(__builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, floatx16{}, 0, 0, 0));
+      for (int t = 0; t < 8; t += 2) {
+        if (t + 2 < 8) a0 = *reinterpret_cast<const half8*>(lda + (t + 2) * 256);
+        const floatx16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b, floatx16{}, 0, 0, 0);
+        if (t + 3 < 8) a1 = *reinterpret_cast<const half8*>(lda + (t + 3) * 256);
+        r0 = fold16(r0, c0);
+        if (t + 2 < 8) c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b, floatx16{}, 0, 0, 0);
+        r1 = fold16(r1, c1);
       }
-      auto mx = [](int x, int y) { return x > y ? x : y; };
-      const int mall = mx(mx(mx(m[0], m[1]), mx(m[2], m[3])), mx(mx(m[4], m[5]), mx(m[6], m[7])));
-      if (__ballot(may_pass(mall, thf)) != 0ull)
-        thf = slow_chunk<C>(lda, b, thf, c * kChunk, nd, gkeys, sm, K, emb, upd);
+      if (__ballot(max(r0, r1) > thi) != 0ull) {
+        if (lane == 0) sm.fired[wave][nfired] = (uint32_t)c;
+        ++nfired;
+      }
+    }
+    const bool window_end = (c_end <= kWarmChunks) || ((g + 1) % kWindowGroups == 0) || (g + 1 == ngroups);
+    if (window_end && nfired > 0) {
+      thf = replay_window<C, STATS>(emb16, b, thf, nfired, nd, gkeys, sm, K, upd, stats);
+      nfired = 0;
     }
   }
 
@@ -503,12 +658,13 @@ __global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* 
     if (qq >= n_active) break;
     const int32_t qid = active[qq];
     uint64_t* kq = gkeys + (size_t)qs * C;
-    compact16<C>(kq, sm, qs, K, emb);
+    compact16<C>(kq, sm, qs, K, emb, STATS ? stats : nullptr);  // exact f32 rescoring of the kept band + sort
     const int n = sm.cnt[qs];
     int32_t* out = cand + (int64_t)qid * K;
     for (int e = lane; e < K; e += 64) out[e] = e < n ? key_idx(kq[e]) : -1;
+    if (lane == 0 && sm.ovf[qs]) ovf_list[atomicAdd(n_ovf, 1)] = qid;
   }
-  if (g_topk_stats) stat_add(6, __builtin_amdgcn_s_memtime() - t_kernel);
+  if (STATS) stat_add(6, __builtin_amdgcn_s_memrealtime() - t_kernel);
 }
 
 template <int C>
@@ -519,7 +675,7 @@ static size_t topk_lds_bytes() {
 template <int C>
 static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, const int32_t* active,
                        const int32_t* n_active, int64_t max_q, int64_t q_offset, int K, int32_t* cand, hipStream_t st,
-                       uint64_t* gkeys, int dbg = 0) {
+                       uint64_t* gkeys, int dbg = 0, unsigned long long* stats = nullptr) {
   const int64_t grid = cdiv(max_q, kTopkQ);
   if (grid == 0) return FWAV_OK;
   if (emb16 != nullptr) {
@@ -527,8 +683,24 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       set_error("fwav_sim_topk: fp16 search needs its key workspace (fwav_sim_topk_workspace_size)");
       return FWAV_ERR_WORKSPACE;
     }
-    k_sim_topk_f16<k16Cap><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(emb16, emb, nd, active, n_active, q_offset, K,
-                                                                       cand, gkeys, dbg);
+    const size_t keys_bytes = (size_t)cdiv(max_q > 0 ? max_q : 1, k16Q) * k16Q * k16Cap * sizeof(uint64_t);
+    int32_t* ovf_list = (int32_t*)((char*)gkeys + keys_bytes);
+    int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
+    (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
+    if (stats != nullptr)
+      k_sim_topk_f16<k16Cap, true><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(
+          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, dbg, stats);
+    else
+      k_sim_topk_f16<k16Cap, false><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(
+          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, nullptr);
+    // queries whose fp16 band overflowed the buffer (none for ordinary audio): exact f32 recompute
+    const size_t lds = topk_lds_bytes<C>();
+    static bool attr32b = false;
+    if (!attr32b) {
+      (void)hipFuncSetAttribute((const void*)k_sim_topk_f32<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr32b = true;
+    }
+    k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, ovf_list, n_ovf, q_offset, K, cand);
   } else {
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32 = false;
@@ -552,7 +724,8 @@ int fwav_topk_max_k(void) { return 64; }
 
 // Global key-buffer workspace of the fp16 search for up to max_q queries (bytes).
 size_t fwav_sim_topk_workspace_size(int64_t max_q) {
-  return (size_t)cdiv(max_q > 0 ? max_q : 1, k16Q) * k16Q * k16Cap * sizeof(uint64_t);
+  const int64_t q = max_q > 0 ? max_q : 1;
+  return (size_t)cdiv(q, k16Q) * k16Q * k16Cap * sizeof(uint64_t) + (size_t)(q + 1) * sizeof(int32_t);
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,
@@ -577,14 +750,8 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t nd, const i
                         int64_t max_q, int64_t q_offset, int K, int32_t* cand, void* workspace, int dbg,
                         unsigned long long* stats, void* stream) {
   FWAV_CHECK_ARG(emb && emb16 && workspace && K >= 1 && K <= 64, FWAV_ERR_ARG, "fwav_debug_sim_topk: bad args");
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_topk_stats), &stats, sizeof(stats), 0, hipMemcpyHostToDevice,
-                               (hipStream_t)stream);
-  int rc = launch_topk<128>(emb, (const _Float16*)emb16, nd, active, n_active, max_q, q_offset, K, cand,
-                            (hipStream_t)stream, (uint64_t*)workspace, dbg);
-  unsigned long long* none = nullptr;
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_topk_stats), &none, sizeof(none), 0, hipMemcpyHostToDevice,
-                               (hipStream_t)stream);
-  return rc;
+  return launch_topk<128>(emb, (const _Float16*)emb16, nd, active, n_active, max_q, q_offset, K, cand,
+                          (hipStream_t)stream, (uint64_t*)workspace, dbg, stats);
 }
 
 }  // extern "C"

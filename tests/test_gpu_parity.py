@@ -157,3 +157,14 @@ def test_f16_prefilter_equals_f32_larger(gen, tile, K):
     a, _ = _cands(sig, tile, K, "f16")
     b, _ = _cands(sig, tile, K, "f32")
     assert np.array_equal(a, b)
+
+
+def test_f16_band_overflow_falls_back_to_exact():
+    """A signal with a 32-sample period makes every domain have ~nd/32 exact duplicates: the fp16 band
+    overflows the key buffer, those queries are recomputed by the f32 kernel — results must stay identical."""
+    n = 24000
+    t = np.arange(n)
+    sig = np.round(8000 * np.sin(2 * np.pi * t / 32) + 3000 * np.sin(2 * np.pi * 3 * t / 32)).astype(np.float32)
+    a, _ = _cands(sig, 1024, 32, "f16")
+    b, _ = _cands(sig, 1024, 32, "f32")
+    assert np.array_equal(a, b)

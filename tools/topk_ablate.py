@@ -27,16 +27,18 @@ n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
 cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
 from fwav._lib import size_call
 wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nr), dtype=torch.uint8, device="cuda")
-stats = torch.zeros(8, dtype=torch.int64, device="cuda")
+stats = torch.zeros(16, dtype=torch.int64, device="cuda")
 call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
      64, cand.data_ptr(), wsk.data_ptr(), 0, stats.data_ptr(), st)
 torch.cuda.synchronize()
 sv = stats.cpu().tolist()
 waves = (nr + 255) // 256 * 8
-print("per wave: slow_chunk calls %.1f, firing tiles %.1f, appends/query %.1f, compactions/query %.2f, "
-      "slow cycles %.3g, compaction cycles %.3g, kernel cycles %.3g" % (sv[0] / waves, sv[1] / waves, sv[2] / nr,
-      sv[3] / nr, sv[4] / waves, sv[5] / waves, sv[6] / waves), flush=True)
-for dbg in [0, 1, 3, 7, 5, 4, 2]:
+us = lambda t: t / 100.0 / waves  # noqa: E731  (100 MHz ticks → µs per wave)
+print("per wave: slow_chunk calls %.1f, firing tiles %.1f, appends/query %.1f, compactions/query %.2f" %
+      (sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr))
+print("per wave µs: kernel %.0f, slow_chunk %.0f, compaction %.0f (drain %.0f, loads %.0f, sort %.0f)" %
+      (us(sv[6]), us(sv[4]), us(sv[5]), us(sv[7]), us(sv[8]), us(sv[9])), flush=True)
+for dbg in [0, 1, 3, 7, 5]:
     for rep in range(2):
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
