@@ -687,7 +687,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     int32_t* ovf_list = (int32_t*)((char*)gkeys + keys_bytes);
     int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
     (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
-    if (stats != nullptr)
+    if (stats != nullptr || dbg != 0)
       k_sim_topk_f16<k16Cap, true><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(
           emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, dbg, stats);
     else

@@ -59,7 +59,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import __graft_entry__
     __graft_entry__.build()
-    from fwav import engine, synth
+    from fwav import api, engine, synth
 
     dev = torch.device("cuda", local)
     cfg = synth.CONFIGS[args.config]
@@ -95,6 +95,36 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+
+    # Host-boundary rate (not `value`): numpy signal in host memory → matches (SoA) back in host memory, i.e.
+    # the compress_audio boundary including PCIe both ways (DESIGN.md "Measurement").
+    def e2e_step():
+        r = engine.compress_device(torch.from_numpy(sig_h).to(dev), tile, K, energy_thresh=1e-4)
+        return [t.cpu() for t in (r.idx, r.s, r.o, r.sym, r.err)]
+
+    e2e_step()
+    torch.cuda.synchronize()
+    te0 = time.perf_counter()
+    for _ in range(max(1, min(args.steps, 3))):
+        e2e_step()
+    e2e_ms = (time.perf_counter() - te0) / max(1, min(args.steps, 3)) * 1e3
+
+    # Decode (the metric's second half, "reconstruction SNR dB"): the reference defaults (8 iterations,
+    # eps 1e-3) and a forced 50-iteration run (eps 0, SURVEY §8(d) cfg5 protocol at this config's size).
+    dec = {}
+    for name, iters, eps in (("default", 8, 1e-3), ("forced50", 50, 0.0)):
+        engine.decompress_device(res.idx, res.s, res.o, res.sym, res.pool, res.n_ranges, res.range_size, iters, eps)
+        torch.cuda.synchronize()
+        td0 = time.perf_counter()
+        rec, ran, _ = engine.decompress_device(res.idx, res.s, res.o, res.sym, res.pool, res.n_ranges,
+                                               res.range_size, iters, eps)
+        torch.cuda.synchronize()
+        tdec = time.perf_counter() - td0
+        snr = api.compute_snr(sig_h, rec[:sig_h.size].cpu().numpy())
+        dec[name] = {"iterations": ran, "ms": tdec * 1e3, "snr_db": snr}
+    nr_, rs_ = res.n_ranges, res.range_size
+    dec["bytes_per_iteration"] = nr_ * (12 * rs_ + 17)  # fwav_decode.hip header
+    dec["iteration_gbs"] = dec["bytes_per_iteration"] / (dec["forced50"]["ms"] * 1e-3 / 50) / 1e9
 
     nr, nd, rs = res.n_ranges, res.n_domains, res.range_size
     n_active = int(res.n_active.item())
@@ -141,6 +171,9 @@ def main():
             "roofline_affine": {"bound": "hbm", "achieved": aff_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": aff_gbs / HBM_PEAK_GBS, "bytes_per_launch": aff_bytes},
             "stage_ms": stage_ms,
+            "host_boundary": {"ms_per_step": e2e_ms, "ranges_per_s": world * nr / (e2e_ms * 1e-3),
+                              "note": "host numpy signal in -> host SoA matches out (PCIe both ways); not `value`"},
+            "decode": dec,
             "cpu_baseline": cpu,
         }
         if cpu and "value" in cpu:
