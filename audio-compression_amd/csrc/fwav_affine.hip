@@ -178,6 +178,129 @@ __global__ __launch_bounds__(64 * kAffWaves) void k_affine_any(const float* __re
   }
 }
 
+
+// ------------------------------------------------------------------ batched kernel (K <= 64, rs 4/8/16)
+// Lane c ↔ candidate c; a wave handles kAffBatch consecutive ranges.  Per range the work is two dependent
+// round trips (candidate row → pool rows) and ~250 VALU ops, so the wave issues all candidate loads of its
+// batch, then all row gathers, then does the math: kAffBatch ranges' latencies overlap and no register is
+// carried across a loop (a software-pipelined persistent loop made the compiler rotate registers and wait
+// for every load at the loop head).  The range samples are wave-uniform (scalar loads).  Both orientations
+// are evaluated together in packed f32 (v_pk_mul_f32 / v_pk_add_f32; each half is one correctly rounded f32
+// op, so the numpy order and results are unchanged) — the VALU is the bound here, at 4 cycles per wave64
+// op.  The argmin is two DPP wave reductions on (NaN-first error order, slot) followed by readlanes of the
+// winner, instead of a 5-value shuffle tree.
+template <int RS>
+__device__ __forceinline__ void gather_row(const float* __restrict__ pool, int32_t ci, float (&D)[RS]) {
+  const int64_t di = ci < 0 ? 0 : ci;
+  if constexpr (RS % 4 == 0) {
+    const float4* p = reinterpret_cast<const float4*>(pool + di * RS);
+#pragma unroll
+    for (int j = 0; j < RS / 4; ++j) {
+      const float4 v = p[j];
+      D[4 * j] = v.x; D[4 * j + 1] = v.y; D[4 * j + 2] = v.z; D[4 * j + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < RS; ++i) D[i] = pool[di * RS + i];
+  }
+}
+
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+
+template <int RS>
+__device__ __forceinline__ void affine_one(const float (&R)[RS], int64_t r, int32_t ci, bool has,
+                                           int K, const float (&D)[RS], float s_clip, int32_t* out_idx,
+                                           float* out_s, float* out_o, uint8_t* out_sym, float* out_err) {
+  const int lane = threadIdx.x & 63;
+  float rc[RS];
+  auto fr = [&](int i) { return R[i]; };
+  const float rm = pw_sum_n<RS>(fr) / (float)RS;
+#pragma unroll
+  for (int i = 0; i < RS; ++i) rc[i] = R[i] - rm;
+
+  // .x = candidate as stored, .y = mirrored
+  f32x2 X[RS];
+#pragma unroll
+  for (int i = 0; i < RS; ++i) X[i] = f32x2{D[i], D[RS - 1 - i]};
+  auto fx = [&](int i) { return X[i]; };
+  const f32x2 dm = pw_sum_n<RS>(fx) / (float)RS;
+  f32x2 dc[RS];
+#pragma unroll
+  for (int i = 0; i < RS; ++i) dc[i] = X[i] - dm;
+  auto fd = [&](int i) { return dc[i] * dc[i]; };
+  const f32x2 den = pw_sum_n<RS>(fd) + 1e-12f;
+  auto fn = [&](int i) { return dc[i] * rc[i]; };
+  const f32x2 num = pw_sum_n<RS>(fn);
+  const f32x2 sv = num / den;
+  const f32x2 ov = rm - sv * dm;
+  auto fe = [&](int i) {
+    const f32x2 df = (sv * X[i] + ov) - R[i];
+    return df * df;
+  };
+  const f32x2 ss = pw_sum_n<RS>(fe);
+  float e0 = sqrtf(ss.x), e1 = sqrtf(ss.y);
+  if (ci < 0) { e0 = INFINITY; e1 = INFINITY; }
+  // lane-local best of slot `lane` and slot K + lane (first minimum, NaN first), then the wave's
+  const bool take1 = better(e1, K + lane, e0, lane);
+  const float eb = take1 ? e1 : e0;
+  const uint32_t slot = take1 ? (uint32_t)(K + lane) : (uint32_t)lane;
+  const uint32_t ekey = has ? ((eb != eb) ? 0u : __float_as_uint(eb) + 1u) : 0xffffffffu;
+  const uint32_t kmin = __ockl_wfred_min_u32(ekey);
+  const uint32_t smin = __ockl_wfred_min_u32((has && ekey == kmin) ? slot : 0xffffffffu);
+  const int wl = (int)(smin < (uint32_t)K ? smin : smin - (uint32_t)K);
+  auto bcast = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), wl)); };
+  const float sb = bcast(take1 ? sv.y : sv.x);
+  const float ob = bcast(take1 ? ov.y : ov.x);
+  const float erb = bcast(eb);
+  const int db = __builtin_amdgcn_readlane(ci < 0 ? 0 : ci, wl);
+  if (lane == 0) {
+    out_idx[r] = db;
+    out_s[r] = clip_sym(sb, fabsf(s_clip));
+    out_o[r] = ob;
+    out_sym[r] = (uint8_t)(smin >= (uint32_t)K);
+    out_err[r] = erb;
+  }
+}
+
+constexpr int kAffBatch = 4;  // ranges per wave in k_affine_batch
+
+template <int RS>
+__global__ __launch_bounds__(64 * kAffWaves) void k_affine_batch(const float* __restrict__ ranges, int64_t nr,
+                                                                 const int32_t* __restrict__ cand, int K,
+                                                                 const float* __restrict__ pool, float s_clip,
+                                                                 int32_t* __restrict__ out_idx,
+                                                                 float* __restrict__ out_s, float* __restrict__ out_o,
+                                                                 uint8_t* __restrict__ out_sym,
+                                                                 float* __restrict__ out_err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * kAffWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t r0 = wave * kAffBatch;
+  if (r0 >= nr) return;
+  const bool has = lane < K;
+  const int lane_c = has ? lane : K - 1;
+  // all candidate loads, then all row gathers, then the math: kAffBatch ranges' round trips overlap
+  int32_t c[kAffBatch];
+#pragma unroll
+  for (int j = 0; j < kAffBatch; ++j) {
+    const int64_t r = r0 + j < nr ? r0 + j : nr - 1;
+    c[j] = cand[r * K + lane_c];
+  }
+  float D[kAffBatch][RS];
+#pragma unroll
+  for (int j = 0; j < kAffBatch; ++j) gather_row<RS>(pool, c[j], D[j]);
+  // range rows: wave-uniform and read-only → constant address space → scalar loads
+  const __attribute__((address_space(4))) float* rg = (const __attribute__((address_space(4))) float*)ranges;
+#pragma unroll
+  for (int j = 0; j < kAffBatch; ++j) {
+    const int64_t r = r0 + j;
+    if (r >= nr) break;
+    float R[RS];
+#pragma unroll
+    for (int i = 0; i < RS; ++i) R[i] = rg[r * RS + i];
+    affine_one<RS>(R, r, has ? c[j] : -1, has, K, D[j], s_clip, out_idx, out_s, out_o, out_sym, out_err);
+  }
+}
+
 }  // namespace fwav
 
 using namespace fwav;
@@ -195,6 +318,21 @@ int fwav_affine(const float* ranges, int64_t nr, int rs, const int32_t* cand, in
   hipStream_t st = (hipStream_t)stream;
   const int64_t grid = cdiv(nr, kAffWaves);
   const int thr = 64 * kAffWaves;
+  if (K <= 64 && (rs == 4 || rs == 8 || rs == 16)) {
+    switch (rs) {
+#define FWAV_AFF_PIPE(RSV)                                                                                   \
+  case RSV:                                                                                                  \
+    k_affine_batch<RSV><<<cdiv(nr, kAffWaves * kAffBatch), thr, 0, st>>>(ranges, nr, cand, K, pool, s_clip,  \
+                                                                         out_idx, out_s, out_o, out_sym, out_err); \
+    break;
+      FWAV_AFF_PIPE(4)
+      FWAV_AFF_PIPE(8)
+      FWAV_AFF_PIPE(16)
+#undef FWAV_AFF_PIPE
+    }
+    FWAV_LAUNCH_CHECK("fwav_affine");
+    return FWAV_OK;
+  }
   switch (rs) {
     case 4: k_affine<4><<<grid, thr, 0, st>>>(ranges, nr, cand, K, pool, s_clip, out_idx, out_s, out_o, out_sym, out_err); break;
     case 8: k_affine<8><<<grid, thr, 0, st>>>(ranges, nr, cand, K, pool, s_clip, out_idx, out_s, out_o, out_sym, out_err); break;

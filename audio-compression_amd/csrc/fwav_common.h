@@ -44,15 +44,18 @@ __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 
 // pairwise_sum (numpy loops_utils.h.src) of f(off .. off+n-1):
 //   n < 8: sequential from 0;  8 <= n <= 128: 8 strided accumulators + tree + sequential tail;
 //   n > 128: split at n2 = n/2 - (n/2)%8 and add the halves.
+// Generic over the element type T = decltype(f(i)): float, or a 2-wide float vector (two independent sums in
+// one packed-f32 instruction stream; each lane of the vector is rounded exactly like the scalar sum).
 template <class F>
-__device__ __forceinline__ float pw_leaf(const F& f, int off, int n) {
+__device__ __forceinline__ auto pw_leaf(const F& f, int off, int n) -> decltype(f(0)) {
+  using T = decltype(f(0));
   if (n < 8) {
-    float r = 0.0f;
+    T r = (T)0.0f;
     for (int i = 0; i < n; ++i) r = r + f(off + i);
     return r;
   }
-  float r0 = f(off + 0), r1 = f(off + 1), r2 = f(off + 2), r3 = f(off + 3);
-  float r4 = f(off + 4), r5 = f(off + 5), r6 = f(off + 6), r7 = f(off + 7);
+  T r0 = f(off + 0), r1 = f(off + 1), r2 = f(off + 2), r3 = f(off + 3);
+  T r4 = f(off + 4), r5 = f(off + 5), r6 = f(off + 6), r7 = f(off + 7);
   const int m = n - (n & 7);
   for (int i = 8; i < m; i += 8) {
     r0 = r0 + f(off + i + 0);
@@ -64,13 +67,13 @@ __device__ __forceinline__ float pw_leaf(const F& f, int off, int n) {
     r6 = r6 + f(off + i + 6);
     r7 = r7 + f(off + i + 7);
   }
-  float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  T res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
   for (int i = m; i < n; ++i) res = res + f(off + i);
   return res;
 }
 
 template <int D, class F>
-__device__ __forceinline__ float pw_rec(const F& f, int off, int n) {
+__device__ __forceinline__ auto pw_rec(const F& f, int off, int n) -> decltype(f(0)) {
   if constexpr (D == 0) {
     return pw_leaf(f, off, n);
   } else {
@@ -84,15 +87,17 @@ __device__ __forceinline__ float pw_rec(const F& f, int off, int n) {
 // np.add.reduce over n <= kMaxPairwise elements: numpy starts the output at 0 (so -0 sums to +0).
 constexpr int kMaxPairwise = 1024;
 template <class F>
-__device__ __forceinline__ float pw_sum(const F& f, int n) {
+__device__ __forceinline__ auto pw_sum(const F& f, int n) -> decltype(f(0)) {
   return 0.0f + pw_rec<3>(f, 0, n);
 }
 
 // Compile-time-length variant (fully unrolled, register-resident operands).
 template <int N, class F>
-__device__ __forceinline__ float pw_sum_n(const F& f) {
+__device__ __forceinline__ auto pw_sum_n(const F& f) -> decltype(f(0)) {
   return 0.0f + pw_rec<3>(f, 0, N);
 }
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // np.clip(x, -c, c) keeps NaN (comparisons false).
 __device__ __forceinline__ float clip_sym(float x, float c) { return x < -c ? -c : (x > c ? c : x); }
