@@ -714,17 +714,25 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
   return FWAV_OK;
 }
 
+// fwav_topk_large.hip (K > 64)
+int64_t large_batch(int64_t nd, int64_t max_q);
+size_t large_workspace_bytes(int64_t nd, int64_t max_q);
+int launch_topk_large(const float* emb, int64_t nd, const int32_t* active, const int32_t* n_active, int64_t max_q,
+                      int64_t q_offset, int K, int32_t* cand, float* S, hipStream_t st);
+
 }  // namespace fwav
 
 using namespace fwav;
 
 extern "C" {
 
-int fwav_topk_max_k(void) { return 64; }
+int fwav_topk_max_k(void) { return 4096; }
 
-// Global key-buffer workspace of the fp16 search for up to max_q queries (bytes).
-size_t fwav_sim_topk_workspace_size(int64_t max_q) {
+// Workspace of fwav_sim_topk: for K <= 64 the fp16 search's global key buffers (max_q queries), for K > 64
+// the score rows of one query batch (≤ 1 GiB).
+size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   const int64_t q = max_q > 0 ? max_q : 1;
+  if (k > 64) return large_workspace_bytes(n_domains, q);
   return (size_t)cdiv(q, k16Q) * k16Q * k16Cap * sizeof(uint64_t) + (size_t)(q + 1) * sizeof(int32_t);
 }
 
@@ -736,10 +744,17 @@ int fwav_sim_topk(const float* emb, const void* emb16, int64_t nd, const int32_t
                   int64_t max_q, int64_t q_offset, int K, int32_t* cand, void* workspace, size_t ws_bytes,
                   void* stream) {
   FWAV_CHECK_ARG(emb && active && n_active && cand && nd > 0 && max_q >= 0, FWAV_ERR_ARG, "fwav_sim_topk: bad args");
-  FWAV_CHECK_ARG(K >= 1 && K <= 64, FWAV_ERR_K, "fwav_sim_topk: K=%d outside [1, 64] (use fwav_sim_topk_large)", K);
+  FWAV_CHECK_ARG(K >= 1 && K <= fwav_topk_max_k(), FWAV_ERR_K, "fwav_sim_topk: K=%d outside [1, %d]", K,
+                 fwav_topk_max_k());
   FWAV_CHECK_ARG(nd < (int64_t)0x7fffffff, FWAV_ERR_SHAPE, "fwav_sim_topk: nd too large");
   hipStream_t st = (hipStream_t)stream;
-  FWAV_CHECK_ARG(emb16 == nullptr || (workspace && ws_bytes >= fwav_sim_topk_workspace_size(max_q)),
+  if (K > 64) {
+    FWAV_CHECK_ARG(workspace && ws_bytes >= fwav_sim_topk_workspace_size(max_q, nd, K), FWAV_ERR_WORKSPACE,
+                   "fwav_sim_topk: workspace too small");
+    if (max_q == 0) return FWAV_OK;
+    return launch_topk_large(emb, nd, active, n_active, max_q, q_offset, K, cand, (float*)workspace, st);
+  }
+  FWAV_CHECK_ARG(emb16 == nullptr || (workspace && ws_bytes >= fwav_sim_topk_workspace_size(max_q, nd, K)),
                  FWAV_ERR_WORKSPACE, "fwav_sim_topk: workspace too small");
   return launch_topk<128>(emb, (const _Float16*)emb16, nd, active, n_active, max_q, q_offset, K, cand, st,
                           (uint64_t*)workspace);

@@ -31,7 +31,7 @@ SIGNATURES = {
     "fwav_pool_workspace_size": (SZ, [I64, I32, I32, I32]),
     "fwav_pool_embed": (I32, [P, I64, I32, I32, I32, P, P, P, P, P, SZ, P]),
     "fwav_topk_max_k": (I32, []),
-    "fwav_sim_topk_workspace_size": (SZ, [I64]),
+    "fwav_sim_topk_workspace_size": (SZ, [I64, I64, I32]),
     "fwav_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, SZ, P]),
     "fwav_debug_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, I32, P, P]),
     "fwav_affine": (I32, [P, I64, I32, P, I32, P, I64, F32, P, P, P, P, P, P]),

@@ -145,7 +145,7 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
     thr32 = F32(energy_thresh)
     lo32 = F32(energy_thresh * 0.5)
     if k > size_call("fwav_topk_max_k"):
-        raise NotImplementedError(f"top_k={k} > {size_call('fwav_topk_max_k')} is not supported by the HIP search")
+        raise ValueError(f"top_k={k} > {size_call('fwav_topk_max_k')} is not supported by the HIP search")
     ws_n = size_call("fwav_voiced_workspace_size", n, frame)
     ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
     ranges = torch.empty(nr * rs, dtype=torch.float32, device=dev)
@@ -193,7 +193,7 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
              emb.data_ptr(), nd, k, cand.data_ptr(), active.data_ptr(), n_active.data_ptr(), st)
         _mark(events, "prune")
         _mark(events, "sim_topk")
-        wk = size_call("fwav_sim_topk_workspace_size", m) if emb16 is not None else 0
+        wk = size_call("fwav_sim_topk_workspace_size", m, nd, k) if (emb16 is not None or k > 64) else 0
         wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
         call("fwav_sim_topk", emb.data_ptr(), _p(emb16), nd, active.data_ptr(), n_active.data_ptr(), m, lo, k,
              cand.data_ptr(), wsk.data_ptr(), wk, st)

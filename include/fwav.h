@@ -76,11 +76,14 @@ int fwav_prune(const float* ranges, int64_t n, int64_t q_offset, int range_size,
  * Replaces range_candidates_from_embedding_emb + pad_candidates (fractal.py:535-552, 617-622): for each
  * local query listed in active[0 .. *n_active) (at most max_q), the K domains with the largest f32 score
  * fma_k(emb[d][k]·emb[q_offset+i][k]) in (score desc, index asc) order, −1-padded when n_domains < K,
- * into cand[i·K .. i·K+K).  emb16 != NULL selects the fp16 MFMA pre-filter + exact f32 rescoring kernel
- * (needs `workspace` of fwav_sim_topk_workspace_size(max_q) bytes); emb16 == NULL runs the all-f32 MFMA
- * kernel.  Both return identical candidates.  1 ≤ K ≤ fwav_topk_max_k(). */
+ * into cand[i·K .. i·K+K).  K ≤ 64: emb16 != NULL selects the fp16 MFMA pre-filter + exact f32 rescoring
+ * kernel, emb16 == NULL the all-f32 MFMA kernel; both return identical candidates.  K > 64 (the module-global
+ * top_k is unrestricted in the reference; K ≥ n_domains returns every domain sorted): batched exact score
+ * rows + per-query select and sort (fwav_topk_large.hip).  `workspace` holds
+ * fwav_sim_topk_workspace_size(max_q, n_domains, k) bytes (unused for K ≤ 64 with emb16 == NULL).
+ * 1 ≤ K ≤ fwav_topk_max_k(). */
 int fwav_topk_max_k(void);
-size_t fwav_sim_topk_workspace_size(int64_t max_q);
+size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k);
 int fwav_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
                   const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand, void* workspace,
                   size_t ws_bytes, void* stream);

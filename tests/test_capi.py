@@ -52,8 +52,13 @@ def test_error_codes_without_gpu(lib):
     rc = L.fwav_sim_topk(None, None, 10, None, None, 10, 0, 64, None, None, 0, None)
     assert rc == -1
     big = ctypes.c_void_p(16)
-    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 4096, big, None, 0, None)
+    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, L.fwav_topk_max_k() + 1, big, None, 0, None)
     assert rc == -3 and b"K=" in L.fwav_last_error()
+    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 0, big, None, 0, None)
+    assert rc == -3
+    # K > 64 needs the score-row workspace
+    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 100, big, None, 0, None)
+    assert rc == -5 and b"workspace" in L.fwav_last_error()
 
 
 def test_embed_tables_match_scipy_dct(lib):
@@ -79,4 +84,8 @@ def test_workspace_sizes(lib):
     assert size_call("fwav_voiced_workspace_size", 2646000, 16) > 0
     assert size_call("fwav_pool_workspace_size", 2646000, 2048, 8, 2) == ((2646000 - 2048) // 2 + 1 + 7 * 128) * 4
     assert size_call("fwav_pool_workspace_size", 1000, 2048, 8, 2) == 0
-    assert size_call("fwav_sim_topk_workspace_size", 330750) >= 330750 * 64 * 8
+    assert size_call("fwav_sim_topk_workspace_size", 330750, 1321977, 64) >= 330750 * 64 * 8
+    # K > 64: one batch of exact score rows, <= 1 GiB, at least one row
+    big = size_call("fwav_sim_topk_workspace_size", 330750, 1321977, 1000)
+    assert 1321977 * 4 <= big <= (1 << 30)
+    assert size_call("fwav_sim_topk_workspace_size", 10, 1000, 1000) == 10 * 1000 * 4

@@ -26,7 +26,7 @@ active = torch.arange(nr, dtype=torch.int32, device="cuda")
 n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
 cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
 from fwav._lib import size_call
-wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nr), dtype=torch.uint8, device="cuda")
+wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nr, nd, 64), dtype=torch.uint8, device="cuda")
 stats = torch.zeros(16, dtype=torch.int64, device="cuda")
 call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
      64, cand.data_ptr(), wsk.data_ptr(), 0, stats.data_ptr(), st)
