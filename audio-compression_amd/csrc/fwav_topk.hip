@@ -242,18 +242,23 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 constexpr float kF16Delta = 2.5e-3f;
 
-// Diagnostic counters (fwav_debug_sim_topk only; stays nullptr in production launches):
-//   [0] slow_chunk calls  [1] firing tiles  [2] appends  [3] compactions
-//   [4] ticks in slow_chunk  [5] ticks in compactions  [6] ticks per wave (whole kernel)
-//   [7] ticks draining stores  [8] ticks loading keys+rows  [9] ticks sorting   (s_memrealtime, 100 MHz)
-#define g_topk_stats stats
+// Diagnostic counters (fwav_debug_sim_topk only; stays nullptr in production launches), summed over waves:
+//   [0] replayed chunks  [1] firing tiles  [2] appends  [3] streaming compactions
+//   [4] ticks in window replays (incl. their compactions)  [5] ticks in streaming compactions
+//   [6] ticks per wave (whole kernel)  [7] ticks waiting at the group barrier  [8] ticks in the final pass
+//   [9] ticks streaming (MFMA + filter, between barrier and window end)  [10] of [5]: store drain
+//   [11] of [5]: sort          (s_memrealtime ticks, 100 MHz)
+// `stats` inside the kernel is the wave's own LDS counter row (lane 0 adds; flushed once per wave at the end),
+// so the instrumentation adds no global atomics to the measured loop.
+constexpr int kStats = 12;
 __device__ __forceinline__ void stat_add_p(unsigned long long* stats, int i, unsigned long long v) {
-  if (stats != nullptr && (threadIdx.x & 63) == 0) atomicAdd(stats + i, v);
+  if (stats != nullptr && (threadIdx.x & 63) == 0) stats[i] += v;
 }
+extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #define stat_add(i, v) stat_add_p(stats, (i), (v))
-constexpr int kGroup = 4;            // chunks per barrier (and per register prefetch group)
-constexpr int k16Waves = 8;
-constexpr int k16Q = 32 * k16Waves;  // queries per workgroup
+constexpr int kGroup = 4;            // production geometry: chunks per barrier (and per register prefetch group)
+constexpr int k16Waves = 8;          // ... waves per workgroup (32 queries each)
+constexpr int k16Q = 32 * k16Waves;  // queries per workgroup (workspace rounding uses this maximum)
 constexpr int k16Threads = 64 * k16Waves;
 constexpr int k16Cap = 256;          // key-buffer entries per query (global workspace)
 constexpr int kWindowGroups = 8;     // after the warm-up, deferred slow work is replayed every 8 groups
@@ -294,59 +299,66 @@ __device__ __forceinline__ bool may_pass(int imx, float thf) {
   return thf < 0.0f || imx > __float_as_int(thf);
 }
 
-struct Topk16Smem {
-  int cnt[k16Q];      // entries in the query's buffer
-  int nex[k16Q];      // final pass: leading entries that are exact
-  float theta[k16Q];  // filter threshold on s16 (append iff s16 > theta)
-  int ovf[k16Q];      // band overflowed the buffer: recompute this query with the f32 kernel
-  int64_t qrow[k16Q];
-  uint32_t fired[k16Waves][kWindowGroups * kGroup];  // per-wave deferred work: chunk indices of a window
+template <int W, int G>
+struct Topk16SmemT {
+  int cnt[32 * W];      // entries in the query's buffer
+  int nex[32 * W];      // final pass: leading entries that are exact
+  float theta[32 * W];  // filter threshold on s16 (append iff s16 > theta)
+  int ovf[32 * W];      // band overflowed the buffer: recompute this query with the f32 kernel
+  int64_t qrow[32 * W];
+  uint32_t fired[W][kWindowGroups * 4];  // per-wave deferred work: chunk indices of a window
+  unsigned long long wstat[W][kStats];   // STATS builds only
 };
 
-// Streaming compaction on fp16-MFMA keys (no f32 rescoring, no table loads): sort the buffer by s16,
-// S16 = K-th largest; every exact top-K member has s16 > S16 − 2δ (K domains have s32 > S16 − δ), so keep
-// exactly that band and filter new domains with it.  If the band would not leave 64 free slots the query
-// is flagged (ovf) and later recomputed by the exact f32 kernel.
-template <int C>
-__device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, Topk16Smem& sm, int ql, int K,
+// Streaming compaction on fp16-MFMA keys (no f32 rescoring, no table loads, no sort): S16 = the K-th largest
+// s16 in the buffer; every exact top-K member has s16 > S16 − 2δ (K domains have s32 > S16 − δ), so keep that
+// band (unsorted; the final pass rescores and sorts) and filter new domains with it.  S16 is only needed as
+// a lower bound at ~2^-11 resolution, so a greedy bitwise radix select over the top 20 bits of the score key
+// finds T ≤ key(S16) with ballots and scalar popcounts (≈ 80 VALU ops, vs ≈ 1,300 + 264 LDS shuffles for a
+// 256-key bitonic sort).  If the band would not leave 64 free slots the query is flagged (ovf) and later
+// recomputed by the exact f32 kernel.
+template <int C, class SM>
+__device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
                                               unsigned long long* stats) {
   constexpr int E = C / 64;
   const unsigned long long t_start = stats ? __builtin_amdgcn_s_memrealtime() : 0;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const unsigned long long t_drained = stats ? __builtin_amdgcn_s_memrealtime() : 0;
   const int n = sm.cnt[ql];
   uint64_t v[E];
+  uint32_t hi[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
     v[j] = e < n ? kq[e] : 0ull;
+    hi[j] = (uint32_t)(v[j] >> 32);  // 0 for empty slots; f2key of any real score is > 0
   }
-  const unsigned long long t_loaded = stats ? __builtin_amdgcn_s_memrealtime() : 0;
-  wave_sort_desc<E>(v);
-  const unsigned long long t_sorted = stats ? __builtin_amdgcn_s_memrealtime() : 0;
-  int m = n;
   float lim = -INFINITY;
   if (n >= K) {
-    const int kl = (K - 1) & 63, kj = (K - 1) >> 6;
-    uint64_t kth = 0;
+    uint32_t T = 0;
+    for (int bit = 31; bit >= 12; --bit) {
+      const uint32_t Tc = T | (1u << bit);
+      int c = 0;
 #pragma unroll
-    for (int j = 0; j < E; ++j)
-      if (j == kj) kth = __shfl(v[j], kl);
-    lim = key_score(kth) - 2.0f * kF16Delta;
-    m = 0;
-#pragma unroll
-    for (int j = 0; j < E; ++j) m += __popcll(__ballot(j * 64 + lane < n && key_score(v[j]) > lim));
+      for (int j = 0; j < E; ++j) c += __popcll(__ballot(hi[j] >= Tc));
+      if (c >= K) T = Tc;
+    }
+    lim = key2f(T) - 2.0f * kF16Delta;
   }
+  // keep: every real entry with s16 > lim, written densely in (j, lane) order
+  int m = 0;
   int ovf = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const bool keep = hi[j] != 0u && key_score(v[j]) > lim;
+    const uint64_t bm = __ballot(keep);
+    const int pos = m + __popcll(bm & ((1ull << lane) - 1ull));
+    if (keep && pos < C - 64) kq[pos] = v[j];
+    m += __popcll(bm);
+  }
   if (m > C - 64) {
     m = C - 64;
     ovf = 1;
-  }
-#pragma unroll
-  for (int j = 0; j < E; ++j) {
-    const int e = j * 64 + lane;
-    if (e < m) kq[e] = v[j];
   }
   if (lane == 0) {
     sm.cnt[ql] = m;
@@ -356,9 +368,6 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, Topk16S
   if (stats) {
     stat_add(3, 1);
     stat_add(5, __builtin_amdgcn_s_memrealtime() - t_start);
-    stat_add(7, t_drained - t_start);
-    stat_add(8, t_loaded - t_drained);
-    stat_add(9, t_sorted - t_loaded);
   }
 }
 
@@ -366,14 +375,12 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, Topk16S
 // Every per-query buffer and counter is owned by one wave, so no cross-wave fences are needed; the wave's
 // own appended stores are drained once (vmcnt(0)), then all key loads and all row loads are issued
 // together (two memory round trips in total).
-template <int C>
-__device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, Topk16Smem& sm, int ql, int K,
+template <int C, class SM>
+__device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
                                           const float* __restrict__ emb, unsigned long long* stats) {
   constexpr int E = C / 64;
-  const unsigned long long t_start = g_topk_stats ? __builtin_amdgcn_s_memrealtime() : 0;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const unsigned long long t_drained = g_topk_stats ? __builtin_amdgcn_s_memrealtime() : 0;
   const int n = sm.cnt[ql];
   const int ne = sm.nex[ql];
   const float4* qp = reinterpret_cast<const float4*>(emb + sm.qrow[ql] * 16);
@@ -420,14 +427,7 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, Topk16Smem&
       }
     }
   }
-  const unsigned long long t_loaded = g_topk_stats ? __builtin_amdgcn_s_memrealtime() : 0;
   wave_sort_desc<E>(v);
-  if (g_topk_stats) {
-    const unsigned long long t_sorted = __builtin_amdgcn_s_memrealtime();
-    stat_add(7, t_drained - t_start);
-    stat_add(8, t_loaded - t_drained);
-    stat_add(9, t_sorted - t_loaded);
-  }
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
@@ -443,10 +443,6 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, Topk16Smem&
     sm.cnt[ql] = m;
     sm.nex[ql] = m;
     sm.theta[ql] = n >= K ? key_score(kth) : -INFINITY;
-  }
-  if (g_topk_stats) {
-    stat_add(3, 1);
-    stat_add(5, __builtin_amdgcn_s_memrealtime() - t_start);
   }
 }
 
@@ -473,9 +469,9 @@ __device__ __forceinline__ int fold16(int r, const floatx16& a) {
 // the survivors (s16 keys) to the wave-owned global key buffers — one LDS atomic per lane per tile
 // reserves the slots; the stores are fire-and-forget — and compact a buffer inline only when it is about
 // to overflow (hard limit).  Ordinary compactions wait for the window end (compact_pending).
-template <int C, bool STATS>
+template <int C, bool STATS, class SM>
 __device__ __forceinline__ float append_tiles(const half8 (&af)[8], half8 b, float thf, int64_t dbase,
-                                              int64_t nd, uint64_t* __restrict__ gkeys, Topk16Smem& sm, int K,
+                                              int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int K,
                                               int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -507,7 +503,7 @@ __device__ __forceinline__ float append_tiles(const half8 (&af)[8], half8 b, flo
       mask &= mask - 1;
       kq[base_i++] = make_key(acc[r], (int32_t)(d0 + (r & 3) + 8 * (r >> 2)));
     }
-    if (STATS && cntm) atomicAdd(stats + 2, (unsigned long long)cntm);
+    if (STATS) stat_add(2, __ockl_wfred_add_u32((uint32_t)cntm));
     uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > C - 32);
     while (need != 0ull) {
       const int l = __builtin_ctzll(need);
@@ -521,9 +517,9 @@ __device__ __forceinline__ float append_tiles(const half8 (&af)[8], half8 b, flo
 
 // Window end: replay the chunks this wave recorded as fired.  Each chunk's 8 fragments are re-read from the
 // fp16 table (L2-resident: streamed at most one window ago) in one batch, then append_tiles runs on them.
-template <int C, bool STATS>
+template <int C, bool STATS, class SM>
 __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int nf,
-                                               int64_t nd, uint64_t* __restrict__ gkeys, Topk16Smem& sm, int K,
+                                               int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int K,
                                                int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -541,8 +537,8 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
 }
 
 // Window end: compact every buffer of this wave that passed the soft limit.
-template <int C, bool STATS>
-__device__ __forceinline__ float compact_pending(float thf, uint64_t* __restrict__ gkeys, Topk16Smem& sm, int K,
+template <int C, bool STATS, class SM>
+__device__ __forceinline__ float compact_pending(float thf, uint64_t* __restrict__ gkeys, SM& sm, int K,
                                                  int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -557,8 +553,8 @@ __device__ __forceinline__ float compact_pending(float thf, uint64_t* __restrict
   return upd ? sm.theta[ql] : thf;
 }
 
-template <int C, bool STATS>
-__global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
+template <int C, bool STATS, int W = k16Waves, int G = kGroup>
+__global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
                                                                 const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
                                                                 const int32_t* __restrict__ n_active_p,
@@ -566,21 +562,28 @@ __global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* 
                                                                 uint64_t* __restrict__ gkeys_all,
                                                                 int32_t* __restrict__ ovf_list,
                                                                 int32_t* __restrict__ n_ovf, int dbg,
-                                                                unsigned long long* stats) {
+                                                                unsigned long long* gstats) {
   // 2 × kGroup chunk slots: a group of kGroup chunks is written, one barrier, then consumed; the next
   // group goes to the other half, so waves may drift up to a group apart between barriers.
-  __shared__ __attribute__((aligned(16))) uint4 slots[2 * kGroup][512];
-  __shared__ Topk16Smem sm;
+  constexpr int kThreads = 64 * W;
+  constexpr int kPer = 512 / kThreads;  // uint4 per thread per 8 KB chunk
+  __shared__ __attribute__((aligned(16))) uint4 slots[2 * G][512];
+  __shared__ Topk16SmemT<W, G> sm;
 
   const int n_active = *n_active_p;
-  const int qbase = blockIdx.x * k16Q;
+  const int qbase = blockIdx.x * 32 * W;
   if (qbase >= n_active) return;
-  uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * k16Q * C;
+  uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * 32 * W * C;
   const unsigned long long t_kernel = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  unsigned long long* stats = nullptr;
+  if (STATS) {
+    if (lane < kStats) sm.wstat[wave][lane] = 0;
+    stats = sm.wstat[wave];
+  }
   const int col = lane & 31;
   const int h = lane >> 5;
   const int ql = wave * 32 + col;
@@ -602,30 +605,37 @@ __global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* 
   }
 
   const int64_t nchunks = cdiv(nd, kChunk);
-  const int64_t ngroups = cdiv(nchunks, kGroup);
+  const int64_t ngroups = cdiv(nchunks, G);
   const uint4* src = reinterpret_cast<const uint4*>(emb16);
-  uint4 pf[kGroup];
+  uint4 pf[G][kPer];
   auto load_group = [&](int64_t g) {
 #pragma unroll
-    for (int j = 0; j < kGroup; ++j) {
-      const int64_t c = g * kGroup + j;
-      pf[j] = (c < nchunks && !(dbg & 4)) ? src[c * 512 + tid] : make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < G; ++j) {
+      const int64_t c = g * G + j;
+#pragma unroll
+      for (int u = 0; u < kPer; ++u)
+        pf[j][u] = (c < nchunks && !(dbg & 4)) ? src[c * 512 + u * kThreads + tid] : make_uint4(0, 0, 0, 0);
     }
   };
   load_group(0);
 
   int nfired = 0;  // wave-uniform count of chunks recorded in sm.fired[wave] this window
   for (int64_t g = 0; g < ngroups; ++g) {
-    uint4(*half)[512] = slots + (g & 1) * kGroup;
+    uint4(*half)[512] = slots + (g & 1) * G;
 #pragma unroll
-    for (int j = 0; j < kGroup; ++j) half[j][tid] = pf[j];
+    for (int j = 0; j < G; ++j)
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) half[j][u * kThreads + tid] = pf[j][u];
     if (g + 1 < ngroups) load_group(g + 1);
+    const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     __syncthreads();
+    const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (STATS) stat_add(7, t_b1 - t_b0);
     if (STATS && (dbg & 2)) continue;
-    const int64_t c_end = (g + 1) * kGroup < nchunks ? (g + 1) * kGroup : nchunks;
+    const int64_t c_end = (g + 1) * G < nchunks ? (g + 1) * G : nchunks;
     int thi = int_threshold(thf);
-    for (int64_t c = g * kGroup; c < c_end; ++c) {
-      const _Float16* lda = reinterpret_cast<const _Float16*>(half[c - g * kGroup]) + ((h * kChunk) + col) * 8;
+    for (int64_t c = g * G; c < c_end; ++c) {
+      const _Float16* lda = reinterpret_cast<const _Float16*>(half[c - g * G]) + ((h * kChunk) + col) * 8;
       // two tiles in flight per wave; every tile folds into one of two running max chains
       int r0 = (int)0x80000000, r1 = (int)0x80000000;
       half8 a0 = *reinterpret_cast<const half8*>(lda + 0 * 256);
@@ -645,12 +655,16 @@ __global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* 
         ++nfired;
       }
     }
-    const bool window_end = (c_end <= kWarmChunks) || ((g + 1) % kWindowGroups == 0) || (g + 1 == ngroups);
+    const unsigned long long t_c = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (STATS) stat_add(9, t_c - t_b1);
+    const bool window_end = (c_end <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
     if (window_end && nfired > 0) {
       thf = replay_window<C, STATS>(emb16, b, thf, nfired, nd, gkeys, sm, K, upd, stats);
       nfired = 0;
+      if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
     }
   }
+  const unsigned long long t_final = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
 
   for (int l = 0; l < 32; ++l) {
     const int qs = wave * 32 + l;
@@ -664,7 +678,11 @@ __global__ __launch_bounds__(k16Threads, 4) void k_sim_topk_f16(const _Float16* 
     for (int e = lane; e < K; e += 64) out[e] = e < n ? key_idx(kq[e]) : -1;
     if (lane == 0 && sm.ovf[qs]) ovf_list[atomicAdd(n_ovf, 1)] = qid;
   }
-  if (STATS) stat_add(6, __builtin_amdgcn_s_memrealtime() - t_kernel);
+  if (STATS) {
+    stat_add(8, __builtin_amdgcn_s_memrealtime() - t_final);
+    stat_add(6, __builtin_amdgcn_s_memrealtime() - t_kernel);
+    if (gstats != nullptr && lane < kStats) atomicAdd(gstats + lane, sm.wstat[wave][lane]);
+  }
 }
 
 template <int C>
@@ -687,12 +705,27 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     int32_t* ovf_list = (int32_t*)((char*)gkeys + keys_bytes);
     int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
     (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
-    if (stats != nullptr || dbg != 0)
-      k_sim_topk_f16<k16Cap, true><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(
-          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, dbg, stats);
-    else
+    if (stats != nullptr || dbg != 0) {
+      // diagnostics: dbg & 7 = ablations (see the kernel), dbg >> 8 = workgroup geometry (waves, chunks/group)
+      switch (dbg >> 8) {
+#define FWAV_GEOM(SEL, W, G)                                                                                   \
+  case SEL:                                                                                                    \
+    k_sim_topk_f16<k16Cap, true, W, G><<<cdiv(max_q, 32 * W), 64 * W, 0, st>>>(                                \
+        emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, dbg & 255, stats);        \
+    break;
+        FWAV_GEOM(1, 4, 2)
+        FWAV_GEOM(2, 4, 4)
+        FWAV_GEOM(3, 8, 2)
+        FWAV_GEOM(4, 2, 2)
+#undef FWAV_GEOM
+        default:
+          k_sim_topk_f16<k16Cap, true><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(
+              emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, dbg & 255, stats);
+      }
+    } else {
       k_sim_topk_f16<k16Cap, false><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(
           emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, nullptr);
+    }
     // queries whose fp16 band overflowed the buffer (none for ordinary audio): exact f32 recompute
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32b = false;

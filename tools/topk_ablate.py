@@ -27,7 +27,7 @@ n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
 cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
 from fwav._lib import size_call
 wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nr, nd, 64), dtype=torch.uint8, device="cuda")
-stats = torch.zeros(16, dtype=torch.int64, device="cuda")
+stats = torch.zeros(16, dtype=torch.int64, device="cuda")  # kStats = 12 used
 call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
      64, cand.data_ptr(), wsk.data_ptr(), 0, stats.data_ptr(), st)
 torch.cuda.synchronize()
@@ -36,9 +36,12 @@ waves = (nr + 255) // 256 * 8
 us = lambda t: t / 100.0 / waves  # noqa: E731  (100 MHz ticks → µs per wave)
 print("per wave: slow_chunk calls %.1f, firing tiles %.1f, appends/query %.1f, compactions/query %.2f" %
       (sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr))
-print("per wave µs: kernel %.0f, slow_chunk %.0f, compaction %.0f (drain %.0f, loads %.0f, sort %.0f)" %
-      (us(sv[6]), us(sv[4]), us(sv[5]), us(sv[7]), us(sv[8]), us(sv[9])), flush=True)
-for dbg in [0, 1, 3, 7, 5]:
+tot = sv[6]
+print("per-wave share of kernel ticks: barrier %.3f, streaming %.3f, replays %.3f (of which compactions %.3f: "
+      "drain %.3f, sort %.3f), final %.3f, other %.3f" %
+      (sv[7] / tot, sv[9] / tot, sv[4] / tot, sv[5] / tot, sv[10] / tot, sv[11] / tot, sv[8] / tot,
+       1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
+for dbg in [0, 1, 3, 7, 5, 0, 1 << 8, 2 << 8, 3 << 8, 4 << 8, 0]:
     for rep in range(2):
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
