@@ -240,6 +240,9 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
 // reduces each tile to its per-lane max (max3 tree) and takes ONE ballot; only when some lane clears
 // θ − δ does it call the out-of-line slow path.
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+// Native 16-byte vector for the chunk stream (a uint4 struct copy lowers to memcpy, which keeps the prefetch
+// array out of registers).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr float kF16Delta = 2.5e-3f;
 
 // Diagnostic counters (fwav_debug_sim_topk only; stays nullptr in production launches), summed over waves:
@@ -324,7 +327,7 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, SM& sm,
   const unsigned long long t_start = stats ? __builtin_amdgcn_s_memrealtime() : 0;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int n = sm.cnt[ql];
+  const int n = min(sm.cnt[ql], C);  // appends past C were dropped and flagged (ovf) by the appender
   uint64_t v[E];
   uint32_t hi[E];
 #pragma unroll
@@ -381,7 +384,7 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
   constexpr int E = C / 64;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int n = sm.cnt[ql];
+  const int n = min(sm.cnt[ql], C);
   const int ne = sm.nex[ql];
   const float4* qp = reinterpret_cast<const float4*>(emb + sm.qrow[ql] * 16);
   uint64_t v[E];
@@ -474,7 +477,7 @@ __device__ __forceinline__ float append_tiles(const half8 (&af)[8], half8 b, flo
                                               int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int K,
                                               int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 31;
   const int h = lane >> 5;
   const int ql = wave * 32 + col;
@@ -522,11 +525,11 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
                                                int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int K,
                                                int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 31;
   const int h = lane >> 5;
   for (int f = 0; f < nf; ++f) {
-    const int64_t c = sm.fired[wave][f];
+    const int64_t c = __builtin_amdgcn_readfirstlane(sm.fired[wave][f]);
     const _Float16* base = emb16 + ((c * 2 + h) * kChunk + col) * 8;
     half8 af[8];
 #pragma unroll
@@ -539,11 +542,11 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
 // Window end: compact every buffer of this wave that passed the soft limit.
 template <int C, bool STATS, class SM>
 __device__ __forceinline__ float compact_pending(float thf, uint64_t* __restrict__ gkeys, SM& sm, int K,
-                                                 int upd, unsigned long long* stats) {
+                                                 int upd, int limit, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ql = wave * 32 + (lane & 31);
-  uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > C / 2);
+  uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > limit);
   if (need == 0ull) return thf;
   while (need != 0ull) {
     const int l = __builtin_ctzll(need);
@@ -563,11 +566,10 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
                                                                 int32_t* __restrict__ ovf_list,
                                                                 int32_t* __restrict__ n_ovf, int dbg,
                                                                 unsigned long long* gstats) {
-  // 2 × kGroup chunk slots: a group of kGroup chunks is written, one barrier, then consumed; the next
-  // group goes to the other half, so waves may drift up to a group apart between barriers.
+  // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
   constexpr int kThreads = 64 * W;
   constexpr int kPer = 512 / kThreads;  // uint4 per thread per 8 KB chunk
-  __shared__ __attribute__((aligned(16))) uint4 slots[2 * G][512];
+  __shared__ __attribute__((aligned(16))) u32x4 slots[2 * G][512];
   __shared__ Topk16SmemT<W, G> sm;
 
   const int n_active = *n_active_p;
@@ -578,7 +580,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: scalar control flow below
   unsigned long long* stats = nullptr;
   if (STATS) {
     if (lane < kStats) sm.wstat[wave][lane] = 0;
@@ -599,40 +601,48 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
   if (h == 0) {
     sm.cnt[ql] = 0;
     sm.nex[ql] = 0;
-    sm.theta[ql] = -INFINITY;
+    sm.theta[ql] = q >= 0 ? -INFINITY : INFINITY;  // slots past n_active never take appends
     sm.ovf[ql] = 0;
     sm.qrow[ql] = qrow;
   }
 
   const int64_t nchunks = cdiv(nd, kChunk);
   const int64_t ngroups = cdiv(nchunks, G);
-  const uint4* src = reinterpret_cast<const uint4*>(emb16);
-  uint4 pf[G][kPer];
-  auto load_group = [&](int64_t g) {
+  const u32x4* src = reinterpret_cast<const u32x4*>(emb16);
+  // Chunk stream: global → LDS directly (global_load_lds_dwordx4: no staging registers, no ds_write).  The
+  // destination of one wave-instruction is wave-uniform base + lane × 16 B, which is exactly the slot layout
+  // (thread t ↔ bytes [16t, 16t + 16) of the 8 KB chunk).  Chunks past the end re-read the last one (never
+  // consumed).  Group g+1 is issued right after the barrier that retires group g and frees its half.
+  auto issue_group = [&](int64_t gg) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-      const int64_t c = g * G + j;
+      int64_t c_ = gg * G + j;
+      c_ = c_ < nchunks ? c_ : nchunks - 1;
+      if (STATS && (dbg & 4)) c_ = 0;  // ablation: no streaming traffic beyond one L2-resident chunk
 #pragma unroll
       for (int u = 0; u < kPer; ++u)
-        pf[j][u] = (c < nchunks && !(dbg & 4)) ? src[c * 512 + u * kThreads + tid] : make_uint4(0, 0, 0, 0);
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src + c_ * 512 + u * kThreads + tid),
+            (__attribute__((address_space(3))) void*)(&slots[(gg & 1) * G + j][u * kThreads + wave * 64]), 16, 0, 0);
     }
   };
-  load_group(0);
+  issue_group(0);
 
   int nfired = 0;  // wave-uniform count of chunks recorded in sm.fired[wave] this window
   for (int64_t g = 0; g < ngroups; ++g) {
-    uint4(*half)[512] = slots + (g & 1) * G;
-#pragma unroll
-    for (int j = 0; j < G; ++j)
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) half[j][u * kThreads + tid] = pf[j][u];
-    if (g + 1 < ngroups) load_group(g + 1);
+    u32x4(*half)[512] = slots + (g & 1) * G;
+    const int64_t c_end = (g + 1) * G < nchunks ? (g + 1) * G : nchunks;
+    const bool window_end = (c_end <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
     const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-    __syncthreads();
+    // RAW: own DMA of group g retired, then every wave's (barrier).  WAR: the other half was last read in
+    // iteration g−1, whose ds_reads were all consumed before its waves reached this barrier.
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(7, t_b1 - t_b0);
+    if (g + 1 < ngroups) issue_group(g + 1);
     if (STATS && (dbg & 2)) continue;
-    const int64_t c_end = (g + 1) * G < nchunks ? (g + 1) * G : nchunks;
     int thi = int_threshold(thf);
     for (int64_t c = g * G; c < c_end; ++c) {
       const _Float16* lda = reinterpret_cast<const _Float16*>(half[c - g * G]) + ((h * kChunk) + col) * 8;
@@ -657,11 +667,13 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     }
     const unsigned long long t_c = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(9, t_c - t_b1);
-    const bool window_end = (c_end <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
-    if (window_end && nfired > 0) {
-      thf = replay_window<C, STATS>(emb16, b, thf, nfired, nd, gkeys, sm, K, upd, stats);
-      nfired = 0;
-      if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
+    if (window_end) {
+      // each wave replays its own fired chunks (compacting inline when a buffer fills)
+      if (nfired > 0) {
+        thf = replay_window<C, STATS>(emb16, b, thf, nfired, nd, gkeys, sm, K, upd, stats);
+        nfired = 0;
+        if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
+      }
     }
   }
   const unsigned long long t_final = STATS ? __builtin_amdgcn_s_memrealtime() : 0;

@@ -37,11 +37,25 @@ us = lambda t: t / 100.0 / waves  # noqa: E731  (100 MHz ticks → µs per wave)
 print("per wave: slow_chunk calls %.1f, firing tiles %.1f, appends/query %.1f, compactions/query %.2f" %
       (sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr))
 tot = sv[6]
-print("per-wave share of kernel ticks: barrier %.3f, streaming %.3f, replays %.3f (of which compactions %.3f: "
-      "drain %.3f, sort %.3f), final %.3f, other %.3f" %
+print("per-wave share of kernel ticks: barrier %.3f, streaming %.3f, replays %.3f (of which compactions %.3f, "
+      "balanced tasks %.3f, post-task barrier %.3f), final %.3f, other %.3f" %
       (sv[7] / tot, sv[9] / tot, sv[4] / tot, sv[5] / tot, sv[10] / tot, sv[11] / tot, sv[8] / tot,
        1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
-for dbg in [0, 1, 3, 7, 5, 0, 1 << 8, 2 << 8, 3 << 8, 4 << 8, 0]:
+for dbg in (16, 1):
+    stats.zero_()
+    call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
+         64, cand.data_ptr(), wsk.data_ptr(), dbg, stats.data_ptr(), st)
+    torch.cuda.synchronize()
+    sv = stats.cpu().tolist()
+    tot = sv[6]
+    keys_bytes = ((nr + 255) // 256) * 256 * 256 * 8
+    n_ovf = int(wsk[keys_bytes + 4 * nr: keys_bytes + 4 * nr + 4].view(torch.int32).item())
+    print("dbg=%d: overflowed queries (f32 recompute) %d" % (dbg, n_ovf))
+    print("dbg=%d: replays/wave %.0f firing tiles/wave %.0f appends/q %.0f compactions/q %.2f | shares: barrier %.3f, "
+          "streaming %.3f, replays %.3f, final %.3f, other %.3f" %
+          (dbg, sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr, sv[7] / tot, sv[9] / tot, sv[4] / tot,
+           sv[8] / tot, 1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
+for dbg in [0, 1, 3, 7, 0]:
     for rep in range(2):
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
