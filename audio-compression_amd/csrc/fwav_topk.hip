@@ -261,8 +261,12 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #define stat_add(i, v) stat_add_p(stats, (i), (v))
 constexpr int kGroup = 4;            // production geometry: chunks per barrier (and per register prefetch group)
 constexpr int k16Waves = 8;          // ... waves per workgroup (32 queries each)
-constexpr int k16Q = 32 * k16Waves;  // queries per workgroup (workspace rounding uses this maximum)
+constexpr int k16Q = 32 * k16Waves;  // queries per workgroup at the largest geometry
 constexpr int k16Threads = 64 * k16Waves;
+// Key-buffer bytes for up to q queries at any geometry (blocks of 32·W queries, W ≤ 8, cover ≤ q + 255).
+__host__ __device__ inline size_t f16_keys_bytes(int64_t q) {
+  return (size_t)(cdiv(q > 0 ? q : 1, 32) * 32 + 256) * 256 /* k16Cap */ * sizeof(uint64_t);
+}
 constexpr int k16Cap = 256;          // key-buffer entries per query (global workspace)
 constexpr int kWindowGroups = 8;     // after the warm-up, deferred slow work is replayed every 8 groups
 constexpr int kWarmChunks = 64;      // ... and after every group during the first 64 chunks
@@ -468,58 +472,53 @@ __device__ __forceinline__ int fold16(int r, const floatx16& a) {
   return m3(r, I(14), I(15));
 }
 
-// Fired chunk (rare after the warm-up): recompute each tile's MFMA from the still-valid LDS slot, append
-// the survivors (s16 keys) to the wave-owned global key buffers — one LDS atomic per lane per tile
-// reserves the slots; the stores are fire-and-forget — and compact a buffer inline only when it is about
-// to overflow (hard limit).  Ordinary compactions wait for the window end (compact_pending).
+// One recomputed tile of a replay (acc = the tile's fp16 MFMA scores, domains dt .. dt+31): append the
+// survivors (s16 keys) to the wave-owned global key buffers — one LDS atomic per lane reserves the slots,
+// the stores are fire-and-forget — and compact a buffer inline only when it is about to overflow.
 template <int C, bool STATS, class SM>
-__device__ __forceinline__ float append_tiles(const half8 (&af)[8], half8 b, float thf, int64_t dbase,
-                                              int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int K,
-                                              int upd, unsigned long long* stats) {
+__device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int64_t dt, int64_t nd,
+                                             uint64_t* __restrict__ gkeys, SM& sm, int K, int upd,
+                                             unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 31;
   const int h = lane >> 5;
   const int ql = wave * 32 + col;
+  if (__ballot(fold16((int)0x80000000, acc) > int_threshold(thf)) == 0ull) return thf;
+  if (STATS) stat_add(1, 1);
   uint64_t* kq = gkeys + (size_t)ql * C;
-  if (STATS) stat_add(0, 1);
-  const bool last = dbase + kChunk > nd;
+  const int64_t d0 = dt + 4 * h;
+  uint32_t mask = 0;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[t], b, floatx16{}, 0, 0, 0);
-    if (__ballot(fold16((int)0x80000000, acc) > int_threshold(thf)) == 0ull) continue;
-    if (STATS) stat_add(1, 1);
-    const int64_t d0 = dbase + t * 32 + 4 * h;
-    uint32_t mask = 0;
+  for (int r = 0; r < 16; ++r) mask |= acc[r] > thf ? (1u << r) : 0u;
+  if (dt + 32 > nd) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) mask |= acc[r] > thf ? (1u << r) : 0u;
-    if (last) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (d0 + (r & 3) + 8 * (r >> 2) >= nd) mask &= ~(1u << r);
-    }
-    const int cntm = __builtin_popcount(mask);
-    int base_i = 0;
-    if (cntm) base_i = atomicAdd(&sm.cnt[ql], cntm);
-    while (mask) {
-      const int r = __builtin_ctz(mask);
-      mask &= mask - 1;
-      kq[base_i++] = make_key(acc[r], (int32_t)(d0 + (r & 3) + 8 * (r >> 2)));
-    }
-    if (STATS) stat_add(2, __ockl_wfred_add_u32((uint32_t)cntm));
-    uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > C - 32);
-    while (need != 0ull) {
-      const int l = __builtin_ctzll(need);
-      need &= need - 1;
-      compact16_s16<C>(gkeys + (size_t)(wave * 32 + l) * C, sm, wave * 32 + l, K, STATS ? stats : nullptr);
-    }
-    if (upd) thf = sm.theta[ql];
+    for (int r = 0; r < 16; ++r)
+      if (d0 + (r & 3) + 8 * (r >> 2) >= nd) mask &= ~(1u << r);
   }
-  return thf;
+  const int cntm = __builtin_popcount(mask);
+  int base_i = 0;
+  if (cntm) base_i = atomicAdd(&sm.cnt[ql], cntm);
+  while (mask) {
+    const int r = __builtin_ctz(mask);
+    mask &= mask - 1;
+    kq[base_i++] = make_key(acc[r], (int32_t)(d0 + (r & 3) + 8 * (r >> 2)));
+  }
+  if (STATS) stat_add(2, __ockl_wfred_add_u32((uint32_t)cntm));
+  uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > C - 32);
+  while (need != 0ull) {
+    const int l = __builtin_ctzll(need);
+    need &= need - 1;
+    compact16_s16<C>(gkeys + (size_t)(wave * 32 + l) * C, sm, wave * 32 + l, K, STATS ? stats : nullptr);
+  }
+  return upd ? sm.theta[ql] : thf;
 }
 
-// Window end: replay the chunks this wave recorded as fired.  Each chunk's 8 fragments are re-read from the
-// fp16 table (L2-resident: streamed at most one window ago) in one batch, then append_tiles runs on them.
+// Window end: replay what this wave recorded.  An entry is (chunk << 4 | chain mask); chain j covers tiles j
+// and j + 4.  The recorded tiles are walked with a wave-uniform cursor in batches of kReplayBatch: all of a
+// batch's fragment loads (from the fp16 table, L2/MALL-resident) are issued together, so a window costs
+// ~one memory round trip per batch instead of one per chunk, and tiles of quiet chains are not recomputed.
+constexpr int kReplayBatch = 8;
 template <int C, bool STATS, class SM>
 __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int nf,
                                                int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int K,
@@ -528,13 +527,42 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 31;
   const int h = lane >> 5;
-  for (int f = 0; f < nf; ++f) {
-    const int64_t c = __builtin_amdgcn_readfirstlane(sm.fired[wave][f]);
-    const _Float16* base = emb16 + ((c * 2 + h) * kChunk + col) * 8;
-    half8 af[8];
+  int i = 0;           // next entry
+  uint32_t rem = 0;    // tiles of the current entry still to replay
+  int64_t cc = 0;      // current entry's chunk
+  if (STATS) stat_add(0, nf);
+  while (true) {
+    int64_t ct[kReplayBatch];  // tile start domain, −1 = none
 #pragma unroll
-    for (int t = 0; t < 8; ++t) af[t] = *reinterpret_cast<const half8*>(base + t * 256);
-    thf = append_tiles<C, STATS>(af, b, thf, c * kChunk, nd, gkeys, sm, K, upd, stats);
+    for (int u = 0; u < kReplayBatch; ++u) {
+      while (rem == 0u && i < nf) {
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane(sm.fired[wave][i++]);
+        cc = e >> 4;
+        rem = (e & 15u) | ((e & 15u) << 4);
+      }
+      if (rem != 0u) {
+        const int t = __builtin_ctz(rem);
+        rem &= rem - 1;
+        ct[u] = cc * kChunk + t * 32;
+      } else {
+        ct[u] = -1;
+      }
+    }
+    if (ct[0] < 0) break;
+    half8 af[kReplayBatch];
+#pragma unroll
+    for (int u = 0; u < kReplayBatch; ++u) {
+      const int64_t dt = ct[u] < 0 ? ct[0] : ct[u];  // unconditional loads (no wait on the spot)
+      const int64_t c = dt / kChunk, t = (dt % kChunk) / 32;
+      af[u] = *reinterpret_cast<const half8*>(emb16 + ((c * 2 + h) * kChunk + col) * 8 + t * 256);
+    }
+#pragma unroll
+    for (int u = 0; u < kReplayBatch; ++u) {
+      if (ct[u] < 0) break;
+      const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], b, floatx16{}, 0, 0, 0);
+      thf = append_tile<C, STATS>(acc, thf, ct[u], nd, gkeys, sm, K, upd, stats);
+    }
+    if (ct[kReplayBatch - 1] < 0) break;
   }
   return thf;
 }
@@ -568,9 +596,15 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
                                                                 unsigned long long* gstats) {
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
   constexpr int kThreads = 64 * W;
-  constexpr int kPer = 512 / kThreads;  // uint4 per thread per 8 KB chunk
-  __shared__ __attribute__((aligned(16))) u32x4 slots[2 * G][512];
-  __shared__ Topk16SmemT<W, G> sm;
+  // ALL of the kernel's LDS is one __shared__ object: beside a second one, hipcc waits vmcnt(0) for the in-flight
+  // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
+  struct Lds {
+    u32x4 slots[2 * G][512];
+    Topk16SmemT<W, G> sm;
+  };
+  __shared__ __attribute__((aligned(16))) Lds lds_all;
+  u32x4(*slots)[512] = lds_all.slots;
+  Topk16SmemT<W, G>& sm = lds_all.sm;
 
   const int n_active = *n_active_p;
   const int qbase = blockIdx.x * 32 * W;
@@ -619,13 +653,23 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
       int64_t c_ = gg * G + j;
       c_ = c_ < nchunks ? c_ : nchunks - 1;
       if (STATS && (dbg & 4)) c_ = 0;  // ablation: no streaming traffic beyond one L2-resident chunk
-#pragma unroll
-      for (int u = 0; u < kPer; ++u)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + c_ * 512 + u * kThreads + tid),
-            (__attribute__((address_space(3))) void*)(&slots[(gg & 1) * G + j][u * kThreads + wave * 64]), 16, 0, 0);
+      if (STATS && (dbg & 128) && (j & 1)) continue;  // ablation: DMA only every other chunk
+      // the chunk's 8 KB = 8 wave-instructions of 64 × 16 B, dealt round-robin over the W waves
+      for (int k = wave; k < 8; k += W) {
+        // inline asm, not the builtin: hipcc would otherwise wait for this DMA (vmcnt(0)) before every ds_read
+        // of the other half; completion is counted by hand at the group top
+        const unsigned lds_dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(
+            (__attribute__((address_space(3))) void*)(&slots[(gg & 1) * G + j][k * 64])));
+        const u32x4* gsrc = src + c_ * 512 + k * 64 + lane;
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+      }
     }
   };
+  // retire the prologue's ordinary loads (query fragment, active list) before the stream, visibly to hipcc
+  // (a load still pending at the loop head is waited on, vmcnt(0), inside every chunk iteration)
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   issue_group(0);
 
   int nfired = 0;  // wave-uniform count of chunks recorded in sm.fired[wave] this window
@@ -646,22 +690,26 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     int thi = int_threshold(thf);
     for (int64_t c = g * G; c < c_end; ++c) {
       const _Float16* lda = reinterpret_cast<const _Float16*>(half[c - g * G]) + ((h * kChunk) + col) * 8;
-      // two tiles in flight per wave; every tile folds into one of two running max chains
-      int r0 = (int)0x80000000, r1 = (int)0x80000000;
+      // two tiles in flight per wave; tile t folds into running max chain t & 3, and each chain takes one
+      // ballot, so a replay recomputes only the tiles (t, t + 4) of the chains that fired
+      int r0 = (int)0x80000000, r1 = (int)0x80000000, r2 = (int)0x80000000, r3 = (int)0x80000000;
       half8 a0 = *reinterpret_cast<const half8*>(lda + 0 * 256);
       half8 a1 = *reinterpret_cast<const half8*>(lda + 1 * 256);
       floatx16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b, floatx16{}, 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < 8; t += 2) {
-        if (t + 2 < 8) a0 = *reinterpret_cast<const half8*>(lda + (t + 2) * 256);
+        const bool halfread = STATS && (dbg & 64);  // ablation: every other fragment read reused
+        if (t + 2 < 8 && !(halfread && (t & 2))) a0 = *reinterpret_cast<const half8*>(lda + (t + 2) * 256);
         const floatx16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b, floatx16{}, 0, 0, 0);
-        if (t + 3 < 8) a1 = *reinterpret_cast<const half8*>(lda + (t + 3) * 256);
-        r0 = fold16(r0, c0);
+        if (t + 3 < 8 && !(halfread && (t & 2))) a1 = *reinterpret_cast<const half8*>(lda + (t + 3) * 256);
+        if ((t & 3) == 0) r0 = fold16(r0, c0); else r2 = fold16(r2, c0);
         if (t + 2 < 8) c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b, floatx16{}, 0, 0, 0);
-        r1 = fold16(r1, c1);
+        if ((t & 3) == 0) r1 = fold16(r1, c1); else r3 = fold16(r3, c1);
       }
-      if (__ballot(max(r0, r1) > thi) != 0ull) {
-        if (lane == 0) sm.fired[wave][nfired] = (uint32_t)c;
+      const uint32_t m4 = (__ballot(r0 > thi) != 0ull ? 1u : 0u) | (__ballot(r1 > thi) != 0ull ? 2u : 0u) |
+                          (__ballot(r2 > thi) != 0ull ? 4u : 0u) | (__ballot(r3 > thi) != 0ull ? 8u : 0u);
+      if (m4 != 0u) {
+        if (lane == 0) sm.fired[wave][nfired] = ((uint32_t)c << 4) | m4;
         ++nfired;
       }
     }
@@ -674,6 +722,10 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
         nfired = 0;
         if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
       }
+      // retire the replay's loads and stores here, visibly to hipcc's wait bookkeeping (vmcnt(0) expcnt(7)
+      // lgkmcnt(15)): otherwise it keeps them "pending" at the loop head and waits on them before the next
+      // chunk's ds_reads — which, at run time, also drains the in-flight chunk DMA
+      __builtin_amdgcn_s_waitcnt(0x0F70);
     }
   }
   const unsigned long long t_final = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -713,31 +765,25 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       set_error("fwav_sim_topk: fp16 search needs its key workspace (fwav_sim_topk_workspace_size)");
       return FWAV_ERR_WORKSPACE;
     }
-    const size_t keys_bytes = (size_t)cdiv(max_q > 0 ? max_q : 1, k16Q) * k16Q * k16Cap * sizeof(uint64_t);
+    const size_t keys_bytes = f16_keys_bytes(max_q);
     int32_t* ovf_list = (int32_t*)((char*)gkeys + keys_bytes);
     int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
     (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
-    if (stats != nullptr || dbg != 0) {
-      // diagnostics: dbg & 7 = ablations (see the kernel), dbg >> 8 = workgroup geometry (waves, chunks/group)
-      switch (dbg >> 8) {
-#define FWAV_GEOM(SEL, W, G)                                                                                   \
-  case SEL:                                                                                                    \
-    k_sim_topk_f16<k16Cap, true, W, G><<<cdiv(max_q, 32 * W), 64 * W, 0, st>>>(                                \
-        emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, dbg & 255, stats);        \
-    break;
-        FWAV_GEOM(1, 4, 2)
-        FWAV_GEOM(2, 4, 4)
-        FWAV_GEOM(3, 8, 2)
-        FWAV_GEOM(4, 2, 2)
-#undef FWAV_GEOM
-        default:
-          k_sim_topk_f16<k16Cap, true><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(
-              emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, dbg & 255, stats);
-      }
+    // Waves per workgroup: 8 (256 queries).  Measured at cfg2: W = 8 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms —
+    // an even 4 waves per SIMD beats a fuller last round of workgroups.  dbg >> 8 forces W (diagnostics).
+    int W = 8;
+    if ((dbg >> 8) >= 6 && (dbg >> 8) <= 8) W = dbg >> 8;
+    const bool st_on = stats != nullptr || (dbg & 255) != 0;
+#define FWAV_F16(WW, STATS_)                                                                                    \
+  k_sim_topk_f16<k16Cap, STATS_, WW, kGroup><<<cdiv(max_q, 32 * WW), 64 * WW, 0, st>>>(                          \
+      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, STATS_ ? (dbg & 255) : 0,      \
+      STATS_ ? stats : nullptr)
+    if (st_on) {
+      if (W == 6) FWAV_F16(6, true); else if (W == 7) FWAV_F16(7, true); else FWAV_F16(8, true);
     } else {
-      k_sim_topk_f16<k16Cap, false><<<cdiv(max_q, k16Q), k16Threads, 0, st>>>(
-          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, nullptr);
+      if (W == 6) FWAV_F16(6, false); else if (W == 7) FWAV_F16(7, false); else FWAV_F16(8, false);
     }
+#undef FWAV_F16
     // queries whose fp16 band overflowed the buffer (none for ordinary audio): exact f32 recompute
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32b = false;
@@ -778,7 +824,7 @@ int fwav_topk_max_k(void) { return 4096; }
 size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   const int64_t q = max_q > 0 ? max_q : 1;
   if (k > 64) return large_workspace_bytes(n_domains, q);
-  return (size_t)cdiv(q, k16Q) * k16Q * k16Cap * sizeof(uint64_t) + (size_t)(q + 1) * sizeof(int32_t);
+  return f16_keys_bytes(q) + (size_t)(q + 1) * sizeof(int32_t);
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,

@@ -55,7 +55,7 @@ for dbg in (16, 1):
           "streaming %.3f, replays %.3f, final %.3f, other %.3f" %
           (dbg, sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr, sv[7] / tot, sv[9] / tot, sv[4] / tot,
            sv[8] / tot, 1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
-for dbg in [0, 1, 3, 7, 0]:
+for dbg in [0, 8 << 8, 7 << 8, 6 << 8, 0, 1]:
     for rep in range(2):
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
