@@ -224,21 +224,27 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
 }
 
 // ------------------------------------------------------------------ fp16 pre-filter + exact f32 rescoring
-// Same contract and results as k_sim_topk_f32.  Scores are first formed by ONE v_mfma_f32_32x32x16_f16 per
-// 32×32 tile from the fp16 copy of the table (vs eight f32 MFMAs).  |s16 − s32| ≤ 2u·‖q‖‖d‖ + f32
-// accumulation error ≤ 1.96e-3 (u = 2^-11, ‖q‖, ‖d‖ ≤ √2), so with δ = 2.5e-3 every domain with
-// s16 ≤ θ − δ has s32 < θ, where θ is the EXACT f32 score of the current K-th best: it cannot enter the
-// top-K and is skipped.  Survivors are appended by index only; when a buffer fills, the wave rescores the
-// not-yet-exact entries in f32 (the f32 MFMA's fma order, k = 0..15; one lane per entry, all loads in
-// flight together), sorts, keeps the top K and sets θ.  Because skipped domains are strictly below θ the
-// result is the exact (score desc, index asc) top-K whatever the processing order.
+// Same contract and results as k_sim_topk_f32 (the production K ≤ 64 search).
 //
-// Geometry: 8 waves × 32 queries per workgroup; the per-query key buffers (C × 8 B) live in a global
-// workspace (touched only on the rare slow path, L2/MALL-resident), so LDS holds just two 8 KB chunk
-// slots + per-query counters (≈ 21 KB) and a CU runs two workgroups = 4 waves per SIMD.  Per chunk (256
-// domains; kGroup chunks per barrier, prefetched a group ahead in registers) each wave issues 8 MFMAs,
-// reduces each tile to its per-lane max (max3 tree) and takes ONE ballot; only when some lane clears
-// θ − δ does it call the out-of-line slow path.
+// Exactness.  Scores are first formed by ONE v_mfma_f32_32x32x16_f16 per 32×32 tile from the fp16 copy of the
+// table.  |s16 − s32| ≤ 2u·‖q‖‖d‖ + f32 accumulation ≤ 1.96e-3 (u = 2^-11, ‖q‖, ‖d‖ ≤ √2) < δ = 2.5e-3.  A
+// query's candidate buffer holds (s16 key, index) pairs; a compaction takes S16 = its K-th largest s16 and keeps
+// the band s16 > S16 − 2δ, which contains every domain that can still be in the exact top K (K domains have
+// s32 > S16 − δ), and new domains are filtered against that band.  The final pass rescores the band in f32
+// (fma chain k = 0..15, the f32 MFMA's order), sorts (score desc, index asc) and emits K — identical to the
+// all-f32 kernel whatever the processing order.  A band that would not leave 64 free slots flags the query
+// for the f32 kernel (periodic signals; never seen on ordinary audio).
+//
+// Geometry.  8 waves × 32 queries per workgroup, two workgroups per CU (4 waves per SIMD).  Lane l owns query
+// l & 31 (the MFMA's B column, in registers for the whole run) and 16 domain rows of each tile.  The fp16
+// table streams through LDS in groups of 4 chunks (256 domains = 8 KB each) with one barrier per group: group
+// g+1 goes global → LDS by LDS-DMA (global_load_lds_dwordx4, 8 wave-instructions per chunk) into the other
+// half while group g is consumed.  Per chunk a wave issues 8 ds_read_b128 + 8 MFMAs and folds each tile's 16
+// outputs into one of 4 running integer-max chains (8 × v_max3 per tile), then takes 4 ballots against its
+// integer filter — one cheap test per 256 domains.  Chunks with a firing chain are recorded (chunk, chain
+// mask) and replayed at the window end (every 32 chunks; every group during the first 64) from L2/MALL in
+// batches of 8 tiles: recompute the tile's MFMA, append survivors (one LDS atomic per lane reserves slots in
+// the query's global key buffer, C = 256 entries), compact a buffer inline when it is nearly full.
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 // Native 16-byte vector for the chunk stream (a uint4 struct copy lowers to memcpy, which keeps the prefetch
 // array out of registers).
@@ -249,8 +255,7 @@ constexpr float kF16Delta = 2.5e-3f;
 //   [0] replayed chunks  [1] firing tiles  [2] appends  [3] streaming compactions
 //   [4] ticks in window replays (incl. their compactions)  [5] ticks in streaming compactions
 //   [6] ticks per wave (whole kernel)  [7] ticks waiting at the group barrier  [8] ticks in the final pass
-//   [9] ticks streaming (MFMA + filter, between barrier and window end)  [10] of [5]: store drain
-//   [11] of [5]: sort          (s_memrealtime ticks, 100 MHz)
+//   [9] ticks streaming (MFMA + filter, between barrier and window end)   (s_memrealtime ticks, 100 MHz)
 // `stats` inside the kernel is the wave's own LDS counter row (lane 0 adds; flushed once per wave at the end),
 // so the instrumentation adds no global atomics to the measured loop.
 constexpr int kStats = 12;
@@ -565,23 +570,6 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
     if (ct[kReplayBatch - 1] < 0) break;
   }
   return thf;
-}
-
-// Window end: compact every buffer of this wave that passed the soft limit.
-template <int C, bool STATS, class SM>
-__device__ __forceinline__ float compact_pending(float thf, uint64_t* __restrict__ gkeys, SM& sm, int K,
-                                                 int upd, int limit, unsigned long long* stats) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ql = wave * 32 + (lane & 31);
-  uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > limit);
-  if (need == 0ull) return thf;
-  while (need != 0ull) {
-    const int l = __builtin_ctzll(need);
-    need &= need - 1;
-    compact16_s16<C>(gkeys + (size_t)(wave * 32 + l) * C, sm, wave * 32 + l, K, STATS ? stats : nullptr);
-  }
-  return upd ? sm.theta[ql] : thf;
 }
 
 template <int C, bool STATS, int W = k16Waves, int G = kGroup>

@@ -1,4 +1,8 @@
-"""Time the similarity search kernel with diagnostic ablations (tools only; outputs are wrong for dbg != 0)."""
+"""Time the similarity search kernel with diagnostic ablations (tools only; outputs are wrong for dbg & 7 != 0).
+
+dbg bits (k_sim_topk_f16, STATS build): 1 = no slow path, 2 = skip MFMA + filter, 4 = no chunk DMA beyond one
+chunk, 64 = reuse every other fragment read, 128 = DMA every other chunk; dbg >> 8 = waves per workgroup (6-8).
+Counters: replayed chunks, firing tiles, appends, compactions, per-segment tick shares, overflow fallbacks."""
 import os, sys, time
 sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                 os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd")]
@@ -37,9 +41,9 @@ us = lambda t: t / 100.0 / waves  # noqa: E731  (100 MHz ticks → µs per wave)
 print("per wave: slow_chunk calls %.1f, firing tiles %.1f, appends/query %.1f, compactions/query %.2f" %
       (sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr))
 tot = sv[6]
-print("per-wave share of kernel ticks: barrier %.3f, streaming %.3f, replays %.3f (of which compactions %.3f, "
-      "balanced tasks %.3f, post-task barrier %.3f), final %.3f, other %.3f" %
-      (sv[7] / tot, sv[9] / tot, sv[4] / tot, sv[5] / tot, sv[10] / tot, sv[11] / tot, sv[8] / tot,
+print("per-wave share of kernel ticks: barrier %.3f, streaming %.3f, replays %.3f (of which compactions %.3f), "
+      "final %.3f, other %.3f" %
+      (sv[7] / tot, sv[9] / tot, sv[4] / tot, sv[5] / tot, sv[8] / tot,
        1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
 for dbg in (16, 1):
     stats.zero_()
