@@ -266,8 +266,6 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #define stat_add(i, v) stat_add_p(stats, (i), (v))
 constexpr int kGroup = 4;            // production geometry: chunks per barrier (and per register prefetch group)
 constexpr int k16Waves = 8;          // ... waves per workgroup (32 queries each)
-constexpr int k16Q = 32 * k16Waves;  // queries per workgroup at the largest geometry
-constexpr int k16Threads = 64 * k16Waves;
 // Key-buffer bytes for up to q queries at any geometry (blocks of 32·W queries, W ≤ 8, cover ≤ q + 255).
 __host__ __device__ inline size_t f16_keys_bytes(int64_t q) {
   return (size_t)(cdiv(q > 0 ? q : 1, 32) * 32 + 256) * 256 /* k16Cap */ * sizeof(uint64_t);
@@ -583,7 +581,6 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
                                                                 int32_t* __restrict__ n_ovf, int dbg,
                                                                 unsigned long long* gstats) {
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
-  constexpr int kThreads = 64 * W;
   // ALL of the kernel's LDS is one __shared__ object: beside a second one, hipcc waits vmcnt(0) for the in-flight
   // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
   struct Lds {
