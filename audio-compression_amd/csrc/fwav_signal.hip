@@ -197,10 +197,17 @@ __global__ void k_prune(const float* __restrict__ ranges, int64_t nr, int64_t q_
     for (int j = 0; j < k; ++j) c[j] = -1;
   } else if (zero) {
     for (int j = 0; j < k; ++j) c[j] = j < nd ? j : -1;
-  } else {
-    int slot = atomicAdd(n_active, 1);
-    active[slot] = (int32_t)i;
   }
+  // append the searchable ranges: one counter atomic per wave (not per range), index order kept within a wave
+  const bool act = !pruned && !zero;
+  const uint64_t m = __ballot(act);
+  if (m == 0ull) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __builtin_ctzll(m);
+  int base = 0;
+  if (lane == leader) base = atomicAdd(n_active, __popcll(m));
+  base = __shfl(base, leader);
+  if (act) active[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
 }
 
 }  // namespace fwav

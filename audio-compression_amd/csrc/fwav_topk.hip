@@ -755,18 +755,18 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
     (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
     // Waves per workgroup: 8 (256 queries).  Measured at cfg2: W = 8 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms —
-    // an even 4 waves per SIMD beats a fuller last round of workgroups.  dbg >> 8 forces W (diagnostics).
+    // an even 4 waves per SIMD beats a fuller last round of workgroups.  dbg >> 8 == 7 forces W = 7 (diagnostics).
     int W = 8;
-    if ((dbg >> 8) >= 6 && (dbg >> 8) <= 8) W = dbg >> 8;
+    if ((dbg >> 8) == 7) W = 7;
     const bool st_on = stats != nullptr || (dbg & 255) != 0;
 #define FWAV_F16(WW, STATS_)                                                                                    \
   k_sim_topk_f16<k16Cap, STATS_, WW, kGroup><<<cdiv(max_q, 32 * WW), 64 * WW, 0, st>>>(                          \
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, STATS_ ? (dbg & 255) : 0,      \
       STATS_ ? stats : nullptr)
     if (st_on) {
-      if (W == 6) FWAV_F16(6, true); else if (W == 7) FWAV_F16(7, true); else FWAV_F16(8, true);
+      if (W == 7) FWAV_F16(7, true); else FWAV_F16(8, true);
     } else {
-      if (W == 6) FWAV_F16(6, false); else if (W == 7) FWAV_F16(7, false); else FWAV_F16(8, false);
+      FWAV_F16(8, false);
     }
 #undef FWAV_F16
     // queries whose fp16 band overflowed the buffer (none for ordinary audio): exact f32 recompute

@@ -53,15 +53,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # FWAV_BENCH_BACKEND=gloo + FWAV_BENCH_SHARE_GPU=1 rehearse the multi-rank path on a one-GPU box (ranks share
+    # cuda:0, collectives on host tensors); the driver's N-GPU runs use the default: RCCL, one GPU per rank.
+    backend = os.environ.get("FWAV_BENCH_BACKEND", "nccl")
+    dev_index = local % torch.cuda.device_count() if os.environ.get("FWAV_BENCH_SHARE_GPU") else local
     if world > 1:
         import torch.distributed as dist  # noqa: F811
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
     import __graft_entry__
     __graft_entry__.build()
     from fwav import api, engine, synth
 
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", dev_index)
     cfg = synth.CONFIGS[args.config]
     sig_h, sr, sw = synth.make_config_signal(args.config, seconds=args.seconds, seed=rank)
     tile, K = cfg["tile"], cfg["top_k"]
@@ -92,7 +99,7 @@ def main():
     t1 = time.perf_counter()
     dt = t1 - t0
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
