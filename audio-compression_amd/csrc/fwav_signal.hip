@@ -175,14 +175,35 @@ __global__ void k_weighted_energy(const float* __restrict__ ranges, int64_t n, d
 //   pruned            → cand row all −1
 //   query row all 0   → cand row 0..min(K,nd)−1 (every score is 0: the (score desc, index asc) order)
 //   otherwise         → appended to `active` for the similarity search
-__global__ void k_prune(const float* __restrict__ ranges, int64_t nr, int64_t q_offset, int rs, float thr,
+// RS > 0: compile-time range size (row in registers, unrolled pairwise sum); RS == 0: runtime rs.
+template <int RS>
+__global__ void k_prune(const float* __restrict__ ranges, int64_t nr, int64_t q_offset, int rs_rt, float thr,
                         int fast_mode, const float* __restrict__ emb, int64_t nd, int k, int32_t* __restrict__ cand,
                         int32_t* __restrict__ active, int32_t* __restrict__ n_active) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nr) return;
+  const int rs = RS > 0 ? RS : rs_rt;
   const float* r = ranges + i * rs;
-  auto sq = [&](int j) { return r[j] * r[j]; };
-  bool pruned = fast_mode && (pw_sum(sq, rs) / (float)rs < thr);
+  float mean_sq;
+  if constexpr (RS > 0) {
+    float v[RS];
+    if constexpr (RS % 4 == 0) {
+#pragma unroll
+      for (int j = 0; j < RS / 4; ++j) {
+        const float4 t = reinterpret_cast<const float4*>(r)[j];
+        v[4 * j] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RS; ++j) v[j] = r[j];
+    }
+    auto sq = [&](int j) { return v[j] * v[j]; };
+    mean_sq = pw_sum_n<RS>(sq) / (float)RS;
+  } else {
+    auto sq = [&](int j) { return r[j] * r[j]; };
+    mean_sq = pw_sum(sq, rs) / (float)rs;
+  }
+  bool pruned = fast_mode && (mean_sq < thr);
   bool zero = true;
   if (!pruned) {
     const float4* q = reinterpret_cast<const float4*>(emb + (i + q_offset) * 16);
@@ -274,8 +295,17 @@ int fwav_prune(const float* ranges, int64_t nr, int64_t q_offset, int rs, float 
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(n_active, 0, sizeof(int32_t), st);
   if (nr == 0) return FWAV_OK;
-  k_prune<<<cdiv(nr, kSignalThreads), kSignalThreads, 0, st>>>(ranges, nr, q_offset, rs, prune_thr, fast_mode, emb,
-                                                                nd, k, cand, active, n_active);
+  const int64_t grid = cdiv(nr, kSignalThreads);
+  switch (rs) {
+#define FWAV_PRUNE(RSV)                                                                                      \
+  k_prune<RSV><<<grid, kSignalThreads, 0, st>>>(ranges, nr, q_offset, rs, prune_thr, fast_mode, emb, nd, k, cand, \
+                                                active, n_active)
+    case 4: FWAV_PRUNE(4); break;
+    case 8: FWAV_PRUNE(8); break;
+    case 16: FWAV_PRUNE(16); break;
+    default: FWAV_PRUNE(0);
+#undef FWAV_PRUNE
+  }
   FWAV_LAUNCH_CHECK("fwav_prune");
   return FWAV_OK;
 }
