@@ -328,13 +328,13 @@ struct Topk16SmemT {
 // 256-key bitonic sort).  If the band would not leave 64 free slots the query is flagged (ovf) and later
 // recomputed by the exact f32 kernel.
 template <int C, class SM>
-__device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
-                                              unsigned long long* stats) {
+__device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n_in, SM& sm, int ql, int K,
+                                              unsigned long long* stats, int& m_out, float& lim_out) {
   constexpr int E = C / 64;
   const unsigned long long t_start = stats ? __builtin_amdgcn_s_memrealtime() : 0;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int n = min(sm.cnt[ql], C);  // appends past C were dropped and flagged (ovf) by the appender
+  const int n = min(n_in, C);
   uint64_t v[E];
   uint32_t hi[E];
 #pragma unroll
@@ -370,11 +370,9 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, SM& sm,
     m = C - 64;
     ovf = 1;
   }
-  if (lane == 0) {
-    sm.cnt[ql] = m;
-    sm.theta[ql] = lim;
-    if (ovf) sm.ovf[ql] = 1;
-  }
+  if (lane == 0 && ovf) sm.ovf[ql] = 1;
+  m_out = m;
+  lim_out = lim;
   if (stats) {
     stat_add(3, 1);
     stat_add(5, __builtin_amdgcn_s_memrealtime() - t_start);
@@ -479,7 +477,7 @@ __device__ __forceinline__ int fold16(int r, const floatx16& a) {
 // survivors (s16 keys) to the wave-owned global key buffers — one LDS atomic per lane reserves the slots,
 // the stores are fire-and-forget — and compact a buffer inline only when it is about to overflow.
 template <int C, bool STATS, class SM>
-__device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int64_t dt, int64_t nd,
+__device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int& qcnt, int64_t dt, int64_t nd,
                                              uint64_t* __restrict__ gkeys, SM& sm, int K, int upd,
                                              unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
@@ -499,22 +497,37 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
     for (int r = 0; r < 16; ++r)
       if (d0 + (r & 3) + 8 * (r >> 2) >= nd) mask &= ~(1u << r);
   }
+  const unsigned long long t_a0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+  // the query's count lives in a register of both its lanes (h = 0, 1): no LDS atomic, no LDS read-back
   const int cntm = __builtin_popcount(mask);
-  int base_i = 0;
-  if (cntm) base_i = atomicAdd(&sm.cnt[ql], cntm);
-  while (mask) {
-    const int r = __builtin_ctz(mask);
-    mask &= mask - 1;
-    kq[base_i++] = make_key(acc[r], (int32_t)(d0 + (r & 3) + 8 * (r >> 2)));
+  const int other = __shfl_xor(cntm, 32);
+  const int base_i = qcnt + (h ? other : 0);
+  qcnt += cntm + other;  // ≤ C: compaction below keeps qcnt ≤ C − 32 before a tile adds ≤ 32
+  // static slots: slot r's key goes to base + popcount of the lower set bits (exec-masked store); faster than a
+  // per-lane ctz loop, whose acc[r] with a per-lane r is a 16-way v_cndmask chain per append
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (mask & (1u << r))
+      kq[base_i + __builtin_popcount(mask & ((1u << r) - 1u))] =
+          make_key(acc[r], (int32_t)(d0 + (r & 3) + 8 * (r >> 2)));
+  if (STATS) {
+    stat_add(2, __ockl_wfred_add_u32((uint32_t)cntm));
+    stat_add(10, __builtin_amdgcn_s_memrealtime() - t_a0);
   }
-  if (STATS) stat_add(2, __ockl_wfred_add_u32((uint32_t)cntm));
-  uint64_t need = __ballot(lane < 32 && sm.cnt[ql] > C - 32);
+  uint64_t need = __ballot(lane < 32 && qcnt > C - 32);
   while (need != 0ull) {
     const int l = __builtin_ctzll(need);
     need &= need - 1;
-    compact16_s16<C>(gkeys + (size_t)(wave * 32 + l) * C, sm, wave * 32 + l, K, STATS ? stats : nullptr);
+    int m;
+    float lim;
+    compact16_s16<C>(gkeys + (size_t)(wave * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l), sm, wave * 32 + l, K,
+                     STATS ? stats : nullptr, m, lim);
+    if (col == l) {
+      qcnt = m;
+      if (upd) thf = lim;
+    }
   }
-  return upd ? sm.theta[ql] : thf;
+  return thf;
 }
 
 // Window end: replay what this wave recorded.  An entry is (chunk << 4 | chain mask); chain j covers tiles j
@@ -523,7 +536,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
 // ~one memory round trip per batch instead of one per chunk, and tiles of quiet chains are not recomputed.
 constexpr int kReplayBatch = 8;
 template <int C, bool STATS, class SM>
-__device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int nf,
+__device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int& qcnt, int nf,
                                                int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int K,
                                                int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
@@ -559,15 +572,62 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
       const int64_t c = dt / kChunk, t = (dt % kChunk) / 32;
       af[u] = *reinterpret_cast<const half8*>(emb16 + ((c * 2 + h) * kChunk + col) * 8 + t * 256);
     }
+    if (STATS) {  // time the fragment round trip (timing build only: forces the wait here)
+      const unsigned long long t_l0 = __builtin_amdgcn_s_memrealtime();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stat_add(11, __builtin_amdgcn_s_memrealtime() - t_l0);
+    }
 #pragma unroll
     for (int u = 0; u < kReplayBatch; ++u) {
       if (ct[u] < 0) break;
       const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], b, floatx16{}, 0, 0, 0);
-      thf = append_tile<C, STATS>(acc, thf, ct[u], nd, gkeys, sm, K, upd, stats);
+      thf = append_tile<C, STATS>(acc, thf, qcnt, ct[u], nd, gkeys, sm, K, upd, stats);
     }
     if (ct[kReplayBatch - 1] < 0) break;
   }
   return thf;
+}
+
+// One full group of NC chunks from the LDS slots, as a single unrolled software pipeline over its 8·NC tiles:
+// fragments are read 3 tiles ahead and each MFMA is issued one tile before its fold, across chunk boundaries
+// (a per-chunk loop waits on its first ds_reads and on its last MFMA at every chunk — half the wave time was
+// parked in those waits).  Tile t of a chunk folds into max chain t & 3; at each chunk end the 4 chains take
+// one ballot each and a firing chunk is recorded as (chunk << 4 | chain mask).
+template <int NC>
+__device__ __forceinline__ int stream_group(const _Float16* __restrict__ lda0, half8 b, int thi, int64_t cbase,
+                                            uint32_t* __restrict__ fired_row, int nfired, int lane) {
+  constexpr int NT = 8 * NC;
+  constexpr int kChunkHalfs = 512 * 8;  // one 8 KB chunk slot
+  auto rd = [&](int i) {
+    return *reinterpret_cast<const half8*>(lda0 + (i >> 3) * kChunkHalfs + (i & 7) * 256);
+  };
+  half8 a[NT];
+  floatx16 acc[NT];
+#pragma unroll
+  for (int i = 0; i < 3 && i < NT; ++i) a[i] = rd(i);
+  acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b, floatx16{}, 0, 0, 0);
+  int r0 = (int)0x80000000, r1 = (int)0x80000000, r2 = (int)0x80000000, r3 = (int)0x80000000;
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    if (i + 3 < NT) a[i + 3] = rd(i + 3);
+    if (i + 1 < NT) acc[i + 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i + 1], b, floatx16{}, 0, 0, 0);
+    switch (i & 3) {
+      case 0: r0 = fold16(r0, acc[i]); break;
+      case 1: r1 = fold16(r1, acc[i]); break;
+      case 2: r2 = fold16(r2, acc[i]); break;
+      default: r3 = fold16(r3, acc[i]); break;
+    }
+    if ((i & 7) == 7) {
+      const uint32_t m4 = (__ballot(r0 > thi) != 0ull ? 1u : 0u) | (__ballot(r1 > thi) != 0ull ? 2u : 0u) |
+                          (__ballot(r2 > thi) != 0ull ? 4u : 0u) | (__ballot(r3 > thi) != 0ull ? 8u : 0u);
+      if (m4 != 0u) {
+        if (lane == 0) fired_row[nfired] = ((uint32_t)(cbase + (i >> 3)) << 4) | m4;
+        ++nfired;
+      }
+      r0 = r1 = r2 = r3 = (int)0x80000000;
+    }
+  }
+  return nfired;
 }
 
 template <int C, bool STATS, int W = k16Waves, int G = kGroup>
@@ -658,6 +718,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
   issue_group(0);
 
   int nfired = 0;  // wave-uniform count of chunks recorded in sm.fired[wave] this window
+  int qcnt = 0;    // entries in this lane's query buffer (same value in both lanes of a query)
   for (int64_t g = 0; g < ngroups; ++g) {
     u32x4(*half)[512] = slots + (g & 1) * G;
     const int64_t c_end = (g + 1) * G < nchunks ? (g + 1) * G : nchunks;
@@ -673,6 +734,10 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     if (g + 1 < ngroups) issue_group(g + 1);
     if (STATS && (dbg & 2)) continue;
     int thi = int_threshold(thf);
+    if (c_end - g * G == G && !(STATS && (dbg & (16 | 64)))) {
+      const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
+      nfired = stream_group<G>(lda0, b, thi, g * G, sm.fired[wave], nfired, lane);
+    } else
     for (int64_t c = g * G; c < c_end; ++c) {
       const _Float16* lda = reinterpret_cast<const _Float16*>(half[c - g * G]) + ((h * kChunk) + col) * 8;
       // two tiles in flight per wave; tile t folds into running max chain t & 3, and each chain takes one
@@ -687,9 +752,17 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
         if (t + 2 < 8 && !(halfread && (t & 2))) a0 = *reinterpret_cast<const half8*>(lda + (t + 2) * 256);
         const floatx16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b, floatx16{}, 0, 0, 0);
         if (t + 3 < 8 && !(halfread && (t & 2))) a1 = *reinterpret_cast<const half8*>(lda + (t + 3) * 256);
-        if ((t & 3) == 0) r0 = fold16(r0, c0); else r2 = fold16(r2, c0);
+        if (STATS && (dbg & 16)) {  // ablation: one max per tile instead of the 16-output fold
+          if ((t & 3) == 0) r0 = max(r0, __float_as_int(c0[0])); else r2 = max(r2, __float_as_int(c0[0]));
+        } else {
+          if ((t & 3) == 0) r0 = fold16(r0, c0); else r2 = fold16(r2, c0);
+        }
         if (t + 2 < 8) c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b, floatx16{}, 0, 0, 0);
-        if ((t & 3) == 0) r1 = fold16(r1, c1); else r3 = fold16(r3, c1);
+        if (STATS && (dbg & 16)) {
+          if ((t & 3) == 0) r1 = max(r1, __float_as_int(c1[0])); else r3 = max(r3, __float_as_int(c1[0]));
+        } else {
+          if ((t & 3) == 0) r1 = fold16(r1, c1); else r3 = fold16(r3, c1);
+        }
       }
       const uint32_t m4 = (__ballot(r0 > thi) != 0ull ? 1u : 0u) | (__ballot(r1 > thi) != 0ull ? 2u : 0u) |
                           (__ballot(r2 > thi) != 0ull ? 4u : 0u) | (__ballot(r3 > thi) != 0ull ? 8u : 0u);
@@ -703,7 +776,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     if (window_end) {
       // each wave replays its own fired chunks (compacting inline when a buffer fills)
       if (nfired > 0) {
-        thf = replay_window<C, STATS>(emb16, b, thf, nfired, nd, gkeys, sm, K, upd, stats);
+        thf = replay_window<C, STATS>(emb16, b, thf, qcnt, nfired, nd, gkeys, sm, K, upd, stats);
         nfired = 0;
         if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
       }
@@ -714,6 +787,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     }
   }
   const unsigned long long t_final = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (h == 0) sm.cnt[ql] = qcnt;  // the final pass reads the counts from LDS (same wave: program order)
 
   for (int l = 0; l < 32; ++l) {
     const int qs = wave * 32 + l;

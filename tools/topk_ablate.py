@@ -41,11 +41,11 @@ us = lambda t: t / 100.0 / waves  # noqa: E731  (100 MHz ticks → µs per wave)
 print("per wave: slow_chunk calls %.1f, firing tiles %.1f, appends/query %.1f, compactions/query %.2f" %
       (sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr))
 tot = sv[6]
-print("per-wave share of kernel ticks: barrier %.3f, streaming %.3f, replays %.3f (of which compactions %.3f), "
-      "final %.3f, other %.3f" %
-      (sv[7] / tot, sv[9] / tot, sv[4] / tot, sv[5] / tot, sv[8] / tot,
+print("per-wave share of kernel ticks: barrier %.3f, streaming %.3f, replays %.3f (of which compactions %.3f, "
+      "appends %.3f, fragment loads %.3f), final %.3f, other %.3f" %
+      (sv[7] / tot, sv[9] / tot, sv[4] / tot, sv[5] / tot, sv[10] / tot, sv[11] / tot, sv[8] / tot,
        1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
-for dbg in (16, 1):
+for dbg in ():
     stats.zero_()
     call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
          64, cand.data_ptr(), wsk.data_ptr(), dbg, stats.data_ptr(), st)
@@ -59,7 +59,7 @@ for dbg in (16, 1):
           "streaming %.3f, replays %.3f, final %.3f, other %.3f" %
           (dbg, sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr, sv[7] / tot, sv[9] / tot, sv[4] / tot,
            sv[8] / tot, 1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
-for dbg in [0, 8 << 8, 7 << 8, 6 << 8, 0, 1]:
+for dbg in [0, 1, 0]:
     for rep in range(2):
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()

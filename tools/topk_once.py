@@ -1,0 +1,37 @@
+"""Run the cfg2 similarity search once (after one warm-up) with a given dbg value — a target for rocprofv3 --pmc.
+usage: python tools/topk_once.py [dbg]"""
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd")]
+import torch
+
+import __graft_entry__
+
+__graft_entry__.build()
+from fwav import engine, synth  # noqa: E402
+from fwav._lib import call, size_call  # noqa: E402
+
+dbg = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+sig = torch.from_numpy(synth.noise(60.0, 44100)).cuda()
+r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
+torch.cuda.synchronize()
+nd, nr = r.n_domains, r.n_ranges
+emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+tab = engine.embed_tables(8, torch.device("cuda"))
+pool = torch.empty(nd * 8, device="cuda")
+emb = torch.empty(nd * 16, device="cuda")
+ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
+     emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+active = torch.arange(nr, dtype=torch.int32, device="cuda")
+n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
+cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
+wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nr, nd, 64), dtype=torch.uint8, device="cuda")
+for _ in range(2):
+    call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
+         64, cand.data_ptr(), wsk.data_ptr(), dbg, None, st)
+torch.cuda.synchronize()
+print("done", dbg)
