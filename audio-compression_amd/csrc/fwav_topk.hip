@@ -271,7 +271,7 @@ __host__ __device__ inline size_t f16_keys_bytes(int64_t q) {
   return (size_t)(cdiv(q > 0 ? q : 1, 32) * 32 + 256) * 256 /* k16Cap */ * sizeof(uint64_t);
 }
 constexpr int k16Cap = 256;          // key-buffer entries per query (global workspace)
-constexpr int kWindowGroups = 8;     // after the warm-up, deferred slow work is replayed every 8 groups
+constexpr int kWindowGroups = 16;    // after the warm-up, fired chunks are replayed every 16 groups (64 chunks)
 constexpr int kWarmChunks = 64;      // ... and after every group during the first 64 chunks
 
 

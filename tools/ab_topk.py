@@ -1,0 +1,61 @@
+"""A/B the similarity search of several libfwav builds in ONE process on the same inputs (interleaved rounds).
+usage: python tools/ab_topk.py lib1.so lib2.so ..."""
+import ctypes as C
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd")]
+import numpy as np
+import torch
+
+import __graft_entry__
+
+__graft_entry__.build()
+from fwav import engine, synth  # noqa: E402
+from fwav._lib import SIGNATURES, size_call  # noqa: E402
+
+libs = []
+for path in sys.argv[1:]:
+    L = C.CDLL(os.path.abspath(path))
+    res, args = SIGNATURES["fwav_sim_topk"]
+    L.fwav_sim_topk.restype, L.fwav_sim_topk.argtypes = res, args
+    libs.append((os.path.basename(path), L))
+sig = torch.from_numpy(synth.noise(60.0, 44100)).cuda()
+r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
+torch.cuda.synchronize()
+nd, nr = r.n_domains, r.n_ranges
+emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+from fwav._lib import call  # noqa: E402
+tab = engine.embed_tables(8, torch.device("cuda"))
+pool = torch.empty(nd * 8, device="cuda")
+emb = torch.empty(nd * 16, device="cuda")
+ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
+     emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+nq = int(os.environ.get("AB_NQ", nr))  # active queries (default: all ranges)
+active = torch.arange(nq, dtype=torch.int32, device="cuda")
+n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
+wsn = size_call("fwav_sim_topk_workspace_size", nr, nd, 64)
+wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
+outs = {}
+times = {n: [] for n, _ in libs}
+for rnd in range(4):
+    for name, L in libs:
+        cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = L.fwav_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0, 64,
+                             cand.data_ptr(), wsk.data_ptr(), wsn, st)
+        e1.record()
+        torch.cuda.synchronize()
+        assert rc == 0, name
+        if rnd > 0:
+            times[name].append(e0.elapsed_time(e1))
+        outs[name] = cand
+ref = outs[libs[0][0]]
+for name, _ in libs:
+    same = bool(torch.equal(outs[name], ref))
+    print(f"{name:24s} median {np.median(times[name]):7.2f} ms  min {min(times[name]):7.2f}  identical={same}", flush=True)
