@@ -264,11 +264,23 @@ __device__ __forceinline__ void stat_add_p(unsigned long long* stats, int i, uns
 }
 extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #define stat_add(i, v) stat_add_p(stats, (i), (v))
-constexpr int kGroup = 4;            // production geometry: chunks per barrier (and per register prefetch group)
-constexpr int k16Waves = 8;          // ... waves per workgroup (32 queries each)
-// Key-buffer bytes for up to q queries at any geometry (blocks of 32·W queries, W ≤ 8, cover ≤ q + 255).
+// Production geometry (the -D overrides build A/B variants: tools/ab_topk.py)
+#ifndef FWAV_TOPK_G
+#define FWAV_TOPK_G 4
+#endif
+#ifndef FWAV_TOPK_W
+#define FWAV_TOPK_W 8
+#endif
+#ifndef FWAV_TOPK_QS
+#define FWAV_TOPK_QS 1
+#endif
+constexpr int kGroup = FWAV_TOPK_G;     // chunks per barrier
+constexpr int k16Waves = FWAV_TOPK_W;   // waves per workgroup
+constexpr int k16Sets = FWAV_TOPK_QS;   // query sets of 32 per wave (each LDS fragment feeds k16Sets MFMAs)
+static_assert(32 * k16Waves * k16Sets <= 512, "f16_keys_bytes covers blocks of at most 512 queries");
+// Key-buffer bytes for up to q queries at any geometry (blocks of 32·W·QS ≤ 512 queries cover ≤ q + 511).
 __host__ __device__ inline size_t f16_keys_bytes(int64_t q) {
-  return (size_t)(cdiv(q > 0 ? q : 1, 32) * 32 + 256) * 256 /* k16Cap */ * sizeof(uint64_t);
+  return (size_t)(cdiv(q > 0 ? q : 1, 32) * 32 + 512) * 256 /* k16Cap */ * sizeof(uint64_t);
 }
 constexpr int k16Cap = 256;          // key-buffer entries per query (global workspace)
 constexpr int kWindowGroups = 16;    // after the warm-up, fired chunks are replayed every 16 groups (64 chunks)
@@ -309,15 +321,15 @@ __device__ __forceinline__ bool may_pass(int imx, float thf) {
   return thf < 0.0f || imx > __float_as_int(thf);
 }
 
-template <int W, int G>
+// NG = query groups of 32 per workgroup (W waves × QS sets).  Kept small: two workgroups (2 × 64 KB of chunk
+// slots + this) must fit one CU's 160 KB of LDS.
+template <int NG, bool STATS>
 struct Topk16SmemT {
-  int cnt[32 * W];      // entries in the query's buffer
-  int nex[32 * W];      // final pass: leading entries that are exact
-  float theta[32 * W];  // filter threshold on s16 (append iff s16 > theta)
-  int ovf[32 * W];      // band overflowed the buffer: recompute this query with the f32 kernel
-  int64_t qrow[32 * W];
-  uint32_t fired[W][kWindowGroups * 4];  // per-wave deferred work: chunk indices of a window
-  unsigned long long wstat[W][kStats];   // STATS builds only
+  int cnt[32 * NG];  // final pass: entries in the query's buffer
+  int ovf[32 * NG];  // band overflowed the buffer: recompute this query with the f32 kernel
+  int64_t qrow[32 * NG];
+  uint32_t fired[NG][kWindowGroups * 4];           // per-group deferred work: chunk indices of a window
+  unsigned long long wstat[STATS ? NG : 1][kStats];  // STATS builds only (one row per wave)
 };
 
 // Streaming compaction on fp16-MFMA keys (no f32 rescoring, no table loads, no sort): S16 = the K-th largest
@@ -379,7 +391,7 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n_i
   }
 }
 
-// Rescore the inexact tail of query ql's buffer kq[0..C), sort, keep the top K, set θ.  Whole wave.
+// Final pass of query ql: rescore its buffer kq[0 .. cnt) in exact f32, sort, keep the top K.  Whole wave.
 // Every per-query buffer and counter is owned by one wave, so no cross-wave fences are needed; the wave's
 // own appended stores are drained once (vmcnt(0)), then all key loads and all row loads are issued
 // together (two memory round trips in total).
@@ -390,7 +402,6 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int n = min(sm.cnt[ql], C);
-  const int ne = sm.nex[ql];
   const float4* qp = reinterpret_cast<const float4*>(emb + sm.qrow[ql] * 16);
   uint64_t v[E];
 #pragma unroll
@@ -404,7 +415,7 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
     const float4 w = qp[i];
     qv[4 * i] = w.x; qv[4 * i + 1] = w.y; qv[4 * i + 2] = w.z; qv[4 * i + 3] = w.w;
   }
-  // rescore the inexact entries two slots at a time (8 row loads in flight per lane)
+  // rescore the entries two slots at a time (8 row loads in flight per lane)
 #pragma unroll
   for (int j0 = 0; j0 < E; j0 += 2) {
     float4 row[2][4];
@@ -413,7 +424,7 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
     for (int jj = 0; jj < 2; ++jj) {
       const int j = j0 + jj;
       const int e = j * 64 + lane;
-      dd[jj] = (j < E && e >= ne && e < n) ? key_idx(v[j < E ? j : 0]) : 0;
+      dd[jj] = (j < E && e < n) ? key_idx(v[j < E ? j : 0]) : 0;
       const float4* p = reinterpret_cast<const float4*>(emb + (int64_t)dd[jj] * 16);
 #pragma unroll
       for (int i = 0; i < 4; ++i) row[jj][i] = p[i];
@@ -422,7 +433,7 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
     for (int jj = 0; jj < 2; ++jj) {
       const int j = j0 + jj;
       const int e = j * 64 + lane;
-      if (j < E && e >= ne && e < n) {
+      if (j < E && e < n) {
         float acc = 0.0f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -441,17 +452,7 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
     const int e = j * 64 + lane;
     if (e < K && e < n) kq[e] = v[j];
   }
-  const int kl = (K - 1) & 63, kj = (K - 1) >> 6;
-  uint64_t kth = 0;
-#pragma unroll
-  for (int j = 0; j < E; ++j)
-    if (j == kj) kth = __shfl(v[j], kl);
-  if (lane == 0) {
-    const int m = n < K ? n : K;
-    sm.cnt[ql] = m;
-    sm.nex[ql] = m;
-    sm.theta[ql] = n >= K ? key_score(kth) : -INFINITY;
-  }
+  if (lane == 0) sm.cnt[ql] = n < K ? n : K;
 }
 
 // Integer filter threshold for the fold-max test: (int)x > thi ⟺ x > thf for non-NaN x when thf >= 0;
@@ -478,13 +479,12 @@ __device__ __forceinline__ int fold16(int r, const floatx16& a) {
 // the stores are fire-and-forget — and compact a buffer inline only when it is about to overflow.
 template <int C, bool STATS, class SM>
 __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int& qcnt, int64_t dt, int64_t nd,
-                                             uint64_t* __restrict__ gkeys, SM& sm, int K, int upd,
+                                             uint64_t* __restrict__ gkeys, SM& sm, int qg, int K, int upd,
                                              unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 31;
   const int h = lane >> 5;
-  const int ql = wave * 32 + col;
+  const int ql = qg * 32 + col;  // qg: the wave-uniform query group (32 queries) of this tile
   if (__ballot(fold16((int)0x80000000, acc) > int_threshold(thf)) == 0ull) return thf;
   if (STATS) stat_add(1, 1);
   uint64_t* kq = gkeys + (size_t)ql * C;
@@ -520,7 +520,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
     need &= need - 1;
     int m;
     float lim;
-    compact16_s16<C>(gkeys + (size_t)(wave * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l), sm, wave * 32 + l, K,
+    compact16_s16<C>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l), sm, qg * 32 + l, K,
                      STATS ? stats : nullptr, m, lim);
     if (col == l) {
       qcnt = m;
@@ -537,10 +537,9 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
 constexpr int kReplayBatch = 8;
 template <int C, bool STATS, class SM>
 __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int& qcnt, int nf,
-                                               int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int K,
+                                               int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int qg, int K,
                                                int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 31;
   const int h = lane >> 5;
   int i = 0;           // next entry
@@ -552,7 +551,7 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
 #pragma unroll
     for (int u = 0; u < kReplayBatch; ++u) {
       while (rem == 0u && i < nf) {
-        const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane(sm.fired[wave][i++]);
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane(sm.fired[qg][i++]);
         cc = e >> 4;
         rem = (e & 15u) | ((e & 15u) << 4);
       }
@@ -581,57 +580,63 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
     for (int u = 0; u < kReplayBatch; ++u) {
       if (ct[u] < 0) break;
       const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], b, floatx16{}, 0, 0, 0);
-      thf = append_tile<C, STATS>(acc, thf, qcnt, ct[u], nd, gkeys, sm, K, upd, stats);
+      thf = append_tile<C, STATS>(acc, thf, qcnt, ct[u], nd, gkeys, sm, qg, K, upd, stats);
     }
     if (ct[kReplayBatch - 1] < 0) break;
   }
   return thf;
 }
 
-// One full group of NC chunks from the LDS slots, as a single unrolled software pipeline over its 8·NC tiles:
-// fragments are read 3 tiles ahead and each MFMA is issued one tile before its fold, across chunk boundaries
-// (a per-chunk loop waits on its first ds_reads and on its last MFMA at every chunk — half the wave time was
-// parked in those waits).  Tile t of a chunk folds into max chain t & 3; at each chunk end the 4 chains take
-// one ballot each and a firing chunk is recorded as (chunk << 4 | chain mask).
-template <int NC>
-__device__ __forceinline__ int stream_group(const _Float16* __restrict__ lda0, half8 b, int thi, int64_t cbase,
-                                            uint32_t* __restrict__ fired_row, int nfired, int lane) {
+// NC chunks from the LDS slots as a single unrolled software pipeline over their 8·NC tiles: fragments are read
+// 3 tiles ahead and each MFMA is issued one tile before its fold, across chunk boundaries (a per-chunk loop waits
+// on its first ds_reads and on its last MFMA at every chunk — half the wave time was parked in those waits).
+// With QS query sets per wave each fragment read feeds QS MFMAs (set s: B operand b[s]).  Tile t of a chunk
+// folds into max chain t & 3 of its set; at each chunk end every chain takes one ballot and a firing chunk is
+// recorded in its set's row as (chunk << 4 | chain mask).
+template <int NC, int QS>
+__device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, const half8 (&b)[QS],
+                                             const int (&thi)[QS], int64_t cbase, uint32_t (*fired)[kWindowGroups * 4],
+                                             int (&nfired)[QS], int lane) {
   constexpr int NT = 8 * NC;
   constexpr int kChunkHalfs = 512 * 8;  // one 8 KB chunk slot
   auto rd = [&](int i) {
     return *reinterpret_cast<const half8*>(lda0 + (i >> 3) * kChunkHalfs + (i & 7) * 256);
   };
   half8 a[NT];
-  floatx16 acc[NT];
+  floatx16 acc[NT][QS];
 #pragma unroll
   for (int i = 0; i < 3 && i < NT; ++i) a[i] = rd(i);
-  acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b, floatx16{}, 0, 0, 0);
-  int r0 = (int)0x80000000, r1 = (int)0x80000000, r2 = (int)0x80000000, r3 = (int)0x80000000;
+#pragma unroll
+  for (int s = 0; s < QS; ++s) acc[0][s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[s], floatx16{}, 0, 0, 0);
+  int r[QS][4];
+#pragma unroll
+  for (int s = 0; s < QS; ++s) r[s][0] = r[s][1] = r[s][2] = r[s][3] = (int)0x80000000;
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     if (i + 3 < NT) a[i + 3] = rd(i + 3);
-    if (i + 1 < NT) acc[i + 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i + 1], b, floatx16{}, 0, 0, 0);
-    switch (i & 3) {
-      case 0: r0 = fold16(r0, acc[i]); break;
-      case 1: r1 = fold16(r1, acc[i]); break;
-      case 2: r2 = fold16(r2, acc[i]); break;
-      default: r3 = fold16(r3, acc[i]); break;
+#pragma unroll
+    for (int s = 0; s < QS; ++s) {
+      if (i + 1 < NT) acc[i + 1][s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i + 1], b[s], floatx16{}, 0, 0, 0);
+      r[s][i & 3] = fold16(r[s][i & 3], acc[i][s]);
     }
     if ((i & 7) == 7) {
-      const uint32_t m4 = (__ballot(r0 > thi) != 0ull ? 1u : 0u) | (__ballot(r1 > thi) != 0ull ? 2u : 0u) |
-                          (__ballot(r2 > thi) != 0ull ? 4u : 0u) | (__ballot(r3 > thi) != 0ull ? 8u : 0u);
-      if (m4 != 0u) {
-        if (lane == 0) fired_row[nfired] = ((uint32_t)(cbase + (i >> 3)) << 4) | m4;
-        ++nfired;
+#pragma unroll
+      for (int s = 0; s < QS; ++s) {
+        const int t = thi[s];
+        const uint32_t m4 = (__ballot(r[s][0] > t) != 0ull ? 1u : 0u) | (__ballot(r[s][1] > t) != 0ull ? 2u : 0u) |
+                            (__ballot(r[s][2] > t) != 0ull ? 4u : 0u) | (__ballot(r[s][3] > t) != 0ull ? 8u : 0u);
+        if (m4 != 0u) {
+          if (lane == 0) fired[s][nfired[s]] = ((uint32_t)(cbase + (i >> 3)) << 4) | m4;
+          ++nfired[s];
+        }
+        r[s][0] = r[s][1] = r[s][2] = r[s][3] = (int)0x80000000;
       }
-      r0 = r1 = r2 = r3 = (int)0x80000000;
     }
   }
-  return nfired;
 }
 
-template <int C, bool STATS, int W = k16Waves, int G = kGroup>
-__global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
+template <int C, bool STATS, int W = k16Waves, int G = kGroup, int QS = k16Sets>
+__global__ __launch_bounds__(64 * W, W / 2) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
                                                                 const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
                                                                 const int32_t* __restrict__ n_active_p,
@@ -640,21 +645,22 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
                                                                 int32_t* __restrict__ ovf_list,
                                                                 int32_t* __restrict__ n_ovf, int dbg,
                                                                 unsigned long long* gstats) {
+  constexpr int NG = W * QS;  // query groups of 32 per workgroup; wave w owns groups w·QS .. w·QS + QS − 1
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
   // ALL of the kernel's LDS is one __shared__ object: beside a second one, hipcc waits vmcnt(0) for the in-flight
   // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
   struct Lds {
     u32x4 slots[2 * G][512];
-    Topk16SmemT<W, G> sm;
+    Topk16SmemT<NG, STATS> sm;
   };
   __shared__ __attribute__((aligned(16))) Lds lds_all;
   u32x4(*slots)[512] = lds_all.slots;
-  Topk16SmemT<W, G>& sm = lds_all.sm;
+  Topk16SmemT<NG, STATS>& sm = lds_all.sm;
 
   const int n_active = *n_active_p;
-  const int qbase = blockIdx.x * 32 * W;
+  const int qbase = blockIdx.x * 32 * NG;
   if (qbase >= n_active) return;
-  uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * 32 * W * C;
+  uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * 32 * NG * C;
   const unsigned long long t_kernel = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
 
   const int tid = threadIdx.x;
@@ -667,22 +673,25 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
   }
   const int col = lane & 31;
   const int h = lane >> 5;
-  const int ql = wave * 32 + col;
-  const int qi = qbase + ql;
-  const int32_t q = qi < n_active ? active[qi] : -1;
-  const int64_t qrow = (int64_t)(q < 0 ? 0 : q) + q_offset;
-  const half8 b = *reinterpret_cast<const half8*>(emb16 + (((qrow >> 8) * 2 + h) * 256 + (qrow & 255)) * 8);
   // dbg (STATS builds only; timing ablations, outputs invalid): 1 = never take the slow path,
-  // 2 = skip MFMA + threshold test, 4 = no global chunk loads
+  // 2 = skip MFMA + threshold test, 4 = no global chunk loads, 128 = DMA only every other chunk
   if (!STATS) dbg = 0;
-  const int upd = (q >= 0 && !(dbg & 1)) ? 1 : 0;
-  float thf = upd ? -INFINITY : INFINITY;
-  if (h == 0) {
-    sm.cnt[ql] = 0;
-    sm.nex[ql] = 0;
-    sm.theta[ql] = q >= 0 ? -INFINITY : INFINITY;  // slots past n_active never take appends
-    sm.ovf[ql] = 0;
-    sm.qrow[ql] = qrow;
+  half8 b[QS];
+  float thf[QS];
+  int upd[QS];
+#pragma unroll
+  for (int s = 0; s < QS; ++s) {
+    const int ql = (wave * QS + s) * 32 + col;
+    const int qi = qbase + ql;
+    const int32_t q = qi < n_active ? active[qi] : -1;
+    const int64_t qrow = (int64_t)(q < 0 ? 0 : q) + q_offset;
+    b[s] = *reinterpret_cast<const half8*>(emb16 + (((qrow >> 8) * 2 + h) * 256 + (qrow & 255)) * 8);
+    upd[s] = (q >= 0 && !(dbg & 1)) ? 1 : 0;
+    thf[s] = upd[s] ? -INFINITY : INFINITY;  // slots past n_active never take appends
+    if (h == 0) {
+      sm.ovf[ql] = 0;
+      sm.qrow[ql] = qrow;
+    }
   }
 
   const int64_t nchunks = cdiv(nd, kChunk);
@@ -712,13 +721,15 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
       }
     }
   };
-  // retire the prologue's ordinary loads (query fragment, active list) before the stream, visibly to hipcc
+  // retire the prologue's ordinary loads (query fragments, active list) before the stream, visibly to hipcc
   // (a load still pending at the loop head is waited on, vmcnt(0), inside every chunk iteration)
   __builtin_amdgcn_s_waitcnt(0x0F70);
   issue_group(0);
 
-  int nfired = 0;  // wave-uniform count of chunks recorded in sm.fired[wave] this window
-  int qcnt = 0;    // entries in this lane's query buffer (same value in both lanes of a query)
+  int nfired[QS];  // wave-uniform counts of chunks recorded in sm.fired[group] this window
+  int qcnt[QS];    // entries in this lane's query buffer (same value in both lanes of a query)
+#pragma unroll
+  for (int s = 0; s < QS; ++s) nfired[s] = qcnt[s] = 0;
   for (int64_t g = 0; g < ngroups; ++g) {
     u32x4(*half)[512] = slots + (g & 1) * G;
     const int64_t c_end = (g + 1) * G < nchunks ? (g + 1) * G : nchunks;
@@ -733,53 +744,29 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     if (STATS) stat_add(7, t_b1 - t_b0);
     if (g + 1 < ngroups) issue_group(g + 1);
     if (STATS && (dbg & 2)) continue;
-    int thi = int_threshold(thf);
-    if (c_end - g * G == G && !(STATS && (dbg & (16 | 64)))) {
-      const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
-      nfired = stream_group<G>(lda0, b, thi, g * G, sm.fired[wave], nfired, lane);
-    } else
-    for (int64_t c = g * G; c < c_end; ++c) {
-      const _Float16* lda = reinterpret_cast<const _Float16*>(half[c - g * G]) + ((h * kChunk) + col) * 8;
-      // two tiles in flight per wave; tile t folds into running max chain t & 3, and each chain takes one
-      // ballot, so a replay recomputes only the tiles (t, t + 4) of the chains that fired
-      int r0 = (int)0x80000000, r1 = (int)0x80000000, r2 = (int)0x80000000, r3 = (int)0x80000000;
-      half8 a0 = *reinterpret_cast<const half8*>(lda + 0 * 256);
-      half8 a1 = *reinterpret_cast<const half8*>(lda + 1 * 256);
-      floatx16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b, floatx16{}, 0, 0, 0);
+    int thi[QS];
 #pragma unroll
-      for (int t = 0; t < 8; t += 2) {
-        const bool halfread = STATS && (dbg & 64);  // ablation: every other fragment read reused
-        if (t + 2 < 8 && !(halfread && (t & 2))) a0 = *reinterpret_cast<const half8*>(lda + (t + 2) * 256);
-        const floatx16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b, floatx16{}, 0, 0, 0);
-        if (t + 3 < 8 && !(halfread && (t & 2))) a1 = *reinterpret_cast<const half8*>(lda + (t + 3) * 256);
-        if (STATS && (dbg & 16)) {  // ablation: one max per tile instead of the 16-output fold
-          if ((t & 3) == 0) r0 = max(r0, __float_as_int(c0[0])); else r2 = max(r2, __float_as_int(c0[0]));
-        } else {
-          if ((t & 3) == 0) r0 = fold16(r0, c0); else r2 = fold16(r2, c0);
-        }
-        if (t + 2 < 8) c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b, floatx16{}, 0, 0, 0);
-        if (STATS && (dbg & 16)) {
-          if ((t & 3) == 0) r1 = max(r1, __float_as_int(c1[0])); else r3 = max(r3, __float_as_int(c1[0]));
-        } else {
-          if ((t & 3) == 0) r1 = fold16(r1, c1); else r3 = fold16(r3, c1);
-        }
-      }
-      const uint32_t m4 = (__ballot(r0 > thi) != 0ull ? 1u : 0u) | (__ballot(r1 > thi) != 0ull ? 2u : 0u) |
-                          (__ballot(r2 > thi) != 0ull ? 4u : 0u) | (__ballot(r3 > thi) != 0ull ? 8u : 0u);
-      if (m4 != 0u) {
-        if (lane == 0) sm.fired[wave][nfired] = ((uint32_t)c << 4) | m4;
-        ++nfired;
-      }
+    for (int s = 0; s < QS; ++s) thi[s] = int_threshold(thf[s]);
+    const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
+    if (c_end - g * G == G) {
+      stream_group<G, QS>(lda0, b, thi, g * G, sm.fired + wave * QS, nfired, lane);
+    } else {
+      for (int64_t c = g * G; c < c_end; ++c)
+        stream_group<1, QS>(lda0 + (c - g * G) * 512 * 8, b, thi, c, sm.fired + wave * QS, nfired, lane);
     }
     const unsigned long long t_c = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(9, t_c - t_b1);
     if (window_end) {
       // each wave replays its own fired chunks (compacting inline when a buffer fills)
-      if (nfired > 0) {
-        thf = replay_window<C, STATS>(emb16, b, thf, qcnt, nfired, nd, gkeys, sm, K, upd, stats);
-        nfired = 0;
-        if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
+#pragma unroll
+      for (int s = 0; s < QS; ++s) {
+        if (nfired[s] > 0) {
+          thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], nfired[s], nd, gkeys, sm, wave * QS + s, K,
+                                           upd[s], stats);
+          nfired[s] = 0;
+        }
       }
+      if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
       // retire the replay's loads and stores here, visibly to hipcc's wait bookkeeping (vmcnt(0) expcnt(7)
       // lgkmcnt(15)): otherwise it keeps them "pending" at the loop head and waits on them before the next
       // chunk's ds_reads — which, at run time, also drains the in-flight chunk DMA
@@ -787,10 +774,13 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     }
   }
   const unsigned long long t_final = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-  if (h == 0) sm.cnt[ql] = qcnt;  // the final pass reads the counts from LDS (same wave: program order)
+  // the final pass reads the counts from LDS (same wave: program order)
+#pragma unroll
+  for (int s = 0; s < QS; ++s)
+    if (h == 0) sm.cnt[(wave * QS + s) * 32 + col] = qcnt[s];
 
-  for (int l = 0; l < 32; ++l) {
-    const int qs = wave * 32 + l;
+  for (int l = 0; l < 32 * QS; ++l) {
+    const int qs = wave * QS * 32 + l;
     const int qq = qbase + qs;
     if (qq >= n_active) break;
     const int32_t qid = active[qq];
@@ -828,21 +818,15 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     int32_t* ovf_list = (int32_t*)((char*)gkeys + keys_bytes);
     int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
     (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
-    // Waves per workgroup: 8 (256 queries).  Measured at cfg2: W = 8 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms —
-    // an even 4 waves per SIMD beats a fuller last round of workgroups.  dbg >> 8 == 7 forces W = 7 (diagnostics).
-    int W = 8;
-    if ((dbg >> 8) == 7) W = 7;
-    const bool st_on = stats != nullptr || (dbg & 255) != 0;
-#define FWAV_F16(WW, STATS_)                                                                                    \
-  k_sim_topk_f16<k16Cap, STATS_, WW, kGroup><<<cdiv(max_q, 32 * WW), 64 * WW, 0, st>>>(                          \
-      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, STATS_ ? (dbg & 255) : 0,      \
-      STATS_ ? stats : nullptr)
-    if (st_on) {
-      if (W == 7) FWAV_F16(7, true); else FWAV_F16(8, true);
-    } else {
-      FWAV_F16(8, false);
-    }
-#undef FWAV_F16
+    // Geometry: k16Waves waves × k16Sets query sets of 32 per workgroup.  Measured at cfg2 (W, QS=1): W = 8
+    // 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms — an even 4 waves per SIMD beats a fuller last round of workgroups.
+    constexpr int NQ = 32 * k16Waves * k16Sets;
+    if (stats != nullptr || (dbg & 255) != 0)
+      k_sim_topk_f16<k16Cap, true><<<cdiv(max_q, NQ), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, dbg & 255, stats);
+    else
+      k_sim_topk_f16<k16Cap, false><<<cdiv(max_q, NQ), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, nullptr);
     // queries whose fp16 band overflowed the buffer (none for ordinary audio): exact f32 recompute
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32b = false;

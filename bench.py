@@ -116,6 +116,18 @@ def main():
         e2e_step()
     e2e_ms = (time.perf_counter() - te0) / max(1, min(args.steps, 3)) * 1e3
 
+    # The reference's own boundary: fractal.compress_audio(numpy signal) -> (MatchList, domains ndarray, ...), i.e.
+    # host signal in, matches + domain pool (nd x rs f32) on the host.
+    sr_api = synth.CONFIGS[args.config]["sr"]
+    api.compress_audio(sig_h, sr_api, 4, tile_size=tile, top_k=K, device=dev)
+    torch.cuda.synchronize()
+    ta0 = time.perf_counter()
+    n_api = max(1, min(args.steps, 3))
+    for _ in range(n_api):
+        out_api = api.compress_audio(sig_h, sr_api, 4, tile_size=tile, top_k=K, device=dev)
+    api_ms = (time.perf_counter() - ta0) / n_api * 1e3
+    assert len(out_api[0]) == out_api[2]
+
     # Decode (the metric's second half, "reconstruction SNR dB"): the reference defaults (8 iterations,
     # eps 1e-3) and a forced 50-iteration run (eps 0, SURVEY §8(d) cfg5 protocol at this config's size).
     dec = {}
@@ -180,6 +192,8 @@ def main():
             "stage_ms": stage_ms,
             "host_boundary": {"ms_per_step": e2e_ms, "ranges_per_s": world * nr / (e2e_ms * 1e-3),
                               "note": "host numpy signal in -> host SoA matches out (PCIe both ways); not `value`"},
+            "api_call": {"ms_per_call": api_ms, "ranges_per_s": world * nr / (api_ms * 1e-3),
+                         "note": "fractal.compress_audio(): host signal in, MatchList + domain pool out; not `value`"},
             "decode": dec,
             "cpu_baseline": cpu,
         }

@@ -1,7 +1,7 @@
 """Time the similarity search kernel with diagnostic ablations (tools only; outputs are wrong for dbg & 7 != 0).
 
 dbg bits (k_sim_topk_f16, STATS build): 1 = no slow path, 2 = skip MFMA + filter, 4 = no chunk DMA beyond one
-chunk, 64 = reuse every other fragment read, 128 = DMA every other chunk; dbg >> 8 = waves per workgroup (6-8).
+chunk, 128 = DMA every other chunk (geometry variants: tools/ab_build.sh + tools/ab_topk.py).
 Counters: replayed chunks, firing tiles, appends, compactions, per-segment tick shares, overflow fallbacks."""
 import os, sys, time
 sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -45,21 +45,21 @@ print("per-wave share of kernel ticks: barrier %.3f, streaming %.3f, replays %.3
       "appends %.3f, fragment loads %.3f), final %.3f, other %.3f" %
       (sv[7] / tot, sv[9] / tot, sv[4] / tot, sv[5] / tot, sv[10] / tot, sv[11] / tot, sv[8] / tot,
        1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
-for dbg in ():
+for dbg in (1, 4):
     stats.zero_()
     call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
          64, cand.data_ptr(), wsk.data_ptr(), dbg, stats.data_ptr(), st)
     torch.cuda.synchronize()
     sv = stats.cpu().tolist()
     tot = sv[6]
-    keys_bytes = ((nr + 255) // 256) * 256 * 256 * 8
+    keys_bytes = (-(-nr // 32) * 32 + 512) * 256 * 8
     n_ovf = int(wsk[keys_bytes + 4 * nr: keys_bytes + 4 * nr + 4].view(torch.int32).item())
     print("dbg=%d: overflowed queries (f32 recompute) %d" % (dbg, n_ovf))
     print("dbg=%d: replays/wave %.0f firing tiles/wave %.0f appends/q %.0f compactions/q %.2f | shares: barrier %.3f, "
           "streaming %.3f, replays %.3f, final %.3f, other %.3f" %
           (dbg, sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr, sv[7] / tot, sv[9] / tot, sv[4] / tot,
            sv[8] / tot, 1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
-for dbg in [0, 1, 0]:
+for dbg in [0, 1, 4, 5, 128, 2, 0]:
     for rep in range(2):
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
