@@ -277,12 +277,39 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 constexpr int kGroup = FWAV_TOPK_G;     // chunks per barrier
 constexpr int k16Waves = FWAV_TOPK_W;   // waves per workgroup
 constexpr int k16Sets = FWAV_TOPK_QS;   // query sets of 32 per wave (each LDS fragment feeds k16Sets MFMAs)
-static_assert(32 * k16Waves * k16Sets <= 512, "f16_keys_bytes covers blocks of at most 512 queries");
-// Key-buffer bytes for up to q queries at any geometry (blocks of 32·W·QS ≤ 512 queries cover ≤ q + 511).
-__host__ __device__ inline size_t f16_keys_bytes(int64_t q) {
-  return (size_t)(cdiv(q > 0 ? q : 1, 32) * 32 + 512) * 256 /* k16Cap */ * sizeof(uint64_t);
-}
 constexpr int k16Cap = 256;          // key-buffer entries per query (global workspace)
+constexpr int k16QB = 32 * k16Waves * k16Sets;  // queries per block (one workgroup's query set)
+constexpr int kMaxPieces = 8;        // a split block's table pieces (merge: P·K ≤ 512 keys per query)
+
+// Work plan of the fp16 search.  The n_blocks query blocks are items of one launch, dispatched in order: the first
+// F = nb − R blocks stream the whole table, then each of the last R = min(nb, rt) blocks is split into P pieces of
+// the table (contiguous chunk ranges) so that the launch's tail is made of short items: without the split the last
+// round of whole-table workgroups runs on a fraction of the slots and takes ≈ 1/5 of the kernel.  A piece ends with
+// its exact top K (f32 keys, sorted), and k_merge_pieces merges a split block's P lists.  Each item owns one
+// key-buffer region (QB queries × C entries).  Every workgroup recomputes the plan from the device-side active
+// count, so the launch needs no host sync; the grid and workspace cover the plan of max_q.
+struct TopkPlan {
+  int64_t nb, F, R;
+  int P;
+  __host__ __device__ int64_t items() const { return F + R * P; }
+};
+__host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P) {
+  TopkPlan pl;
+  pl.nb = cdiv(n_queries > 0 ? n_queries : 0, k16QB);
+  pl.P = P < 1 ? 1 : (P > kMaxPieces ? kMaxPieces : P);
+  pl.R = pl.P == 1 ? 0 : (pl.nb < rt ? pl.nb : (int64_t)rt);
+  pl.F = pl.nb - pl.R;
+  return pl;
+}
+// item → (block, piece, pieces)
+__host__ __device__ inline void plan_item(const TopkPlan& pl, int64_t item, int64_t& block, int& piece, int& np) {
+  if (item < pl.F) {
+    block = item; piece = 0; np = 1;
+  } else {
+    const int64_t j = item - pl.F;
+    block = pl.F + j / pl.P; piece = (int)(j % pl.P); np = pl.P;
+  }
+}
 constexpr int kWindowGroups = 16;    // after the warm-up, fired chunks are replayed every 16 groups (64 chunks)
 constexpr int kWarmChunks = 64;      // ... and after every group during the first 64 chunks
 
@@ -593,10 +620,12 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
 // With QS query sets per wave each fragment read feeds QS MFMAs (set s: B operand b[s]).  Tile t of a chunk
 // folds into max chain t & 3 of its set; at each chunk end every chain takes one ballot and a firing chunk is
 // recorded in its set's row as (chunk << 4 | chain mask).
-template <int NC, int QS>
+// MODE (timing ablations, STATS builds only): 1 = fold but no ballots/records, 2 = MFMA with a 2-output fold
+// (one v_max3 per tile instead of 8; results kept alive through `sink`).
+template <int NC, int QS, int MODE = 0>
 __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, const half8 (&b)[QS],
                                              const int (&thi)[QS], int64_t cbase, uint32_t (*fired)[kWindowGroups * 4],
-                                             int (&nfired)[QS], int lane) {
+                                             int (&nfired)[QS], int lane, int* sink = nullptr) {
   constexpr int NT = 8 * NC;
   constexpr int kChunkHalfs = 512 * 8;  // one 8 KB chunk slot
   auto rd = [&](int i) {
@@ -617,7 +646,17 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
 #pragma unroll
     for (int s = 0; s < QS; ++s) {
       if (i + 1 < NT) acc[i + 1][s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i + 1], b[s], floatx16{}, 0, 0, 0);
-      r[s][i & 3] = fold16(r[s][i & 3], acc[i][s]);
+      if (MODE & 2)
+        r[s][i & 3] = max(max(r[s][i & 3], __float_as_int(acc[i][s][0])), __float_as_int(acc[i][s][15]));
+      else
+        r[s][i & 3] = fold16(r[s][i & 3], acc[i][s]);
+    }
+    if (MODE != 0) {
+      if (i == NT - 1) {
+#pragma unroll
+        for (int s = 0; s < QS; ++s) *sink ^= r[s][0] ^ r[s][1] ^ r[s][2] ^ r[s][3];
+      }
+      continue;
     }
     if ((i & 7) == 7) {
 #pragma unroll
@@ -636,15 +675,15 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
 }
 
 template <int C, bool STATS, int W = k16Waves, int G = kGroup, int QS = k16Sets>
-__global__ __launch_bounds__(64 * W, W / 2) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
+__global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
                                                                 const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
                                                                 const int32_t* __restrict__ n_active_p,
                                                                 int64_t q_offset, int K, int32_t* __restrict__ cand,
                                                                 uint64_t* __restrict__ gkeys_all,
                                                                 int32_t* __restrict__ ovf_list,
-                                                                int32_t* __restrict__ n_ovf, int dbg,
-                                                                unsigned long long* gstats) {
+                                                                int32_t* __restrict__ n_ovf, int plan_rt,
+                                                                int plan_p, int dbg, unsigned long long* gstats) {
   constexpr int NG = W * QS;  // query groups of 32 per workgroup; wave w owns groups w·QS .. w·QS + QS − 1
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
   // ALL of the kernel's LDS is one __shared__ object: beside a second one, hipcc waits vmcnt(0) for the in-flight
@@ -658,9 +697,13 @@ __global__ __launch_bounds__(64 * W, W / 2) void k_sim_topk_f16(const _Float16* 
   Topk16SmemT<NG, STATS>& sm = lds_all.sm;
 
   const int n_active = *n_active_p;
-  const int qbase = blockIdx.x * 32 * NG;
-  if (qbase >= n_active) return;
-  uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * 32 * NG * C;
+  const TopkPlan plan = make_plan(n_active, plan_rt, plan_p);
+  int64_t block;
+  int piece, npieces;
+  plan_item(plan, blockIdx.x, block, piece, npieces);
+  if (block >= plan.nb) return;
+  const int qbase = (int)(block * 32 * NG);
+  uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * 32 * NG * C;  // this item's key-buffer region
   const unsigned long long t_kernel = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
 
   const int tid = threadIdx.x;
@@ -674,7 +717,9 @@ __global__ __launch_bounds__(64 * W, W / 2) void k_sim_topk_f16(const _Float16* 
   const int col = lane & 31;
   const int h = lane >> 5;
   // dbg (STATS builds only; timing ablations, outputs invalid): 1 = never take the slow path,
-  // 2 = skip MFMA + threshold test, 4 = no global chunk loads, 128 = DMA only every other chunk
+  // 2 = skip MFMA + threshold test, 4 = no global chunk loads, 128 = DMA only every other chunk,
+  // 256 = no group barrier, 512 = fold without ballots, 1024 = MFMA without fold, 4096 = record the workgroup
+  // timeline (combinable with the others)
   if (!STATS) dbg = 0;
   half8 b[QS];
   float thf[QS];
@@ -695,7 +740,9 @@ __global__ __launch_bounds__(64 * W, W / 2) void k_sim_topk_f16(const _Float16* 
   }
 
   const int64_t nchunks = cdiv(nd, kChunk);
-  const int64_t ngroups = cdiv(nchunks, G);
+  // this item's chunk range [c0, c1) (the whole table unless the block is split)
+  const int64_t c0 = nchunks * piece / npieces, c1 = nchunks * (piece + 1) / npieces;
+  const int64_t ngroups = cdiv(c1 - c0, G);
   const u32x4* src = reinterpret_cast<const u32x4*>(emb16);
   // Chunk stream: global → LDS directly (global_load_lds_dwordx4: no staging registers, no ds_write).  The
   // destination of one wave-instruction is wave-uniform base + lane × 16 B, which is exactly the slot layout
@@ -704,8 +751,8 @@ __global__ __launch_bounds__(64 * W, W / 2) void k_sim_topk_f16(const _Float16* 
   auto issue_group = [&](int64_t gg) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-      int64_t c_ = gg * G + j;
-      c_ = c_ < nchunks ? c_ : nchunks - 1;
+      int64_t c_ = c0 + gg * G + j;
+      c_ = c_ < c1 ? c_ : c1 - 1;
       if (STATS && (dbg & 4)) c_ = 0;  // ablation: no streaming traffic beyond one L2-resident chunk
       if (STATS && (dbg & 128) && (j & 1)) continue;  // ablation: DMA only every other chunk
       // the chunk's 8 KB = 8 wave-instructions of 64 × 16 B, dealt round-robin over the W waves
@@ -724,22 +771,26 @@ __global__ __launch_bounds__(64 * W, W / 2) void k_sim_topk_f16(const _Float16* 
   // retire the prologue's ordinary loads (query fragments, active list) before the stream, visibly to hipcc
   // (a load still pending at the loop head is waited on, vmcnt(0), inside every chunk iteration)
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  issue_group(0);
+  if (ngroups > 0) issue_group(0);
 
+  int sink = 0;     // ablation builds: keeps the MFMA / fold results of dbg 512/1024 alive
   int nfired[QS];  // wave-uniform counts of chunks recorded in sm.fired[group] this window
   int qcnt[QS];    // entries in this lane's query buffer (same value in both lanes of a query)
 #pragma unroll
   for (int s = 0; s < QS; ++s) nfired[s] = qcnt[s] = 0;
   for (int64_t g = 0; g < ngroups; ++g) {
     u32x4(*half)[512] = slots + (g & 1) * G;
-    const int64_t c_end = (g + 1) * G < nchunks ? (g + 1) * G : nchunks;
-    const bool window_end = (c_end <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
+    const int64_t cg = c0 + g * G;  // first chunk of group g
+    const int64_t c_end = cg + G < c1 ? cg + G : c1;
+    const bool window_end = (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
     const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     // RAW: own DMA of group g retired, then every wave's (barrier).  WAR: the other half was last read in
     // iteration g−1, whose ds_reads were all consumed before its waves reached this barrier.
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    if (!(STATS && (dbg & 256))) {  // ablation 256: no group barrier (LDS races; timing only)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
     const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(7, t_b1 - t_b0);
     if (g + 1 < ngroups) issue_group(g + 1);
@@ -748,11 +799,17 @@ __global__ __launch_bounds__(64 * W, W / 2) void k_sim_topk_f16(const _Float16* 
 #pragma unroll
     for (int s = 0; s < QS; ++s) thi[s] = int_threshold(thf[s]);
     const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
-    if (c_end - g * G == G) {
-      stream_group<G, QS>(lda0, b, thi, g * G, sm.fired + wave * QS, nfired, lane);
+    if (STATS && (dbg & (512 | 1024)) && c_end - cg == G) {
+      // ablations 512: fold without ballots, 1024: MFMA without fold (outputs invalid)
+      if (dbg & 1024)
+        stream_group<G, QS, 2>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane, &sink);
+      else
+        stream_group<G, QS, 1>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane, &sink);
+    } else if (c_end - cg == G) {
+      stream_group<G, QS>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
     } else {
-      for (int64_t c = g * G; c < c_end; ++c)
-        stream_group<1, QS>(lda0 + (c - g * G) * 512 * 8, b, thi, c, sm.fired + wave * QS, nfired, lane);
+      for (int64_t c = cg; c < c_end; ++c)
+        stream_group<1, QS>(lda0 + (c - cg) * 512 * 8, b, thi, c, sm.fired + wave * QS, nfired, lane);
     }
     const unsigned long long t_c = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(9, t_c - t_b1);
@@ -787,15 +844,122 @@ __global__ __launch_bounds__(64 * W, W / 2) void k_sim_topk_f16(const _Float16* 
     uint64_t* kq = gkeys + (size_t)qs * C;
     compact16<C>(kq, sm, qs, K, emb, STATS ? stats : nullptr);  // exact f32 rescoring of the kept band + sort
     const int n = sm.cnt[qs];
-    int32_t* out = cand + (int64_t)qid * K;
-    for (int e = lane; e < K; e += 64) out[e] = e < n ? key_idx(kq[e]) : -1;
-    if (lane == 0 && sm.ovf[qs]) ovf_list[atomicAdd(n_ovf, 1)] = qid;
+    if (npieces == 1) {
+      int32_t* out = cand + (int64_t)qid * K;
+      for (int e = lane; e < K; e += 64) out[e] = e < n ? key_idx(kq[e]) : -1;
+      if (lane == 0 && sm.ovf[qs]) ovf_list[atomicAdd(n_ovf, 1)] = qid;
+    } else {
+      // a piece: its exact top K stays in the buffer as sorted f32 keys (0-padded), the overflow flag in the
+      // last entry; k_merge_pieces combines the block's pieces
+      for (int e = n + lane; e < K; e += 64) kq[e] = 0ull;
+      if (lane == 0) kq[C - 1] = sm.ovf[qs] ? 1ull : 0ull;
+    }
   }
   if (STATS) {
+    if (sink == 0x7fffffff) cand[0] = sink;
     stat_add(8, __builtin_amdgcn_s_memrealtime() - t_final);
     stat_add(6, __builtin_amdgcn_s_memrealtime() - t_kernel);
     if (gstats != nullptr && lane < kStats) atomicAdd(gstats + lane, sm.wstat[wave][lane]);
+    // dbg 4096: workgroup timeline (start of its first wave, end of its last) at gstats[16 + 2·block]
+    if (gstats != nullptr && (dbg & 4096) && lane == 0) {
+      atomicMin(gstats + 16 + 2 * blockIdx.x, t_kernel);
+      atomicMax(gstats + 17 + 2 * blockIdx.x, __builtin_amdgcn_s_memrealtime());
+    }
   }
+}
+
+// Merge the pieces of split blocks: per query, the P sorted exact top-K key lists of its block's pieces → the
+// top K of their union (the top K of a union is the top K of the parts' top Ks), ties by index as everywhere.
+// One wave per query; a query flagged by any piece goes to the f32 recompute list once.
+template <int C>
+__global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
+                                                      const int32_t* __restrict__ active,
+                                                      const int32_t* __restrict__ n_active_p, int plan_rt, int plan_p,
+                                                      int K, int32_t* __restrict__ cand, int32_t* __restrict__ ovf_list,
+                                                      int32_t* __restrict__ n_ovf) {
+  constexpr int E = kMaxPieces;  // ≤ 8 pieces × K ≤ 64 keys = 512 = 8 per lane
+  const int n_active = *n_active_p;
+  const TopkPlan plan = make_plan(n_active, plan_rt, plan_p);
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // split-block query index
+  if (plan.R == 0 || w >= plan.R * k16QB) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t block = plan.F + w / k16QB;
+  const int ql = (int)(w % k16QB);
+  const int64_t qq = block * k16QB + ql;
+  if (qq >= n_active) return;
+  const int P = plan.P;
+  uint64_t v[E];
+  int flag = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    // slot j·64 + lane ↔ piece (j·64 + lane) / K, entry (j·64 + lane) % K
+    const int e = j * 64 + lane;
+    const int p = e / K, r = e % K;
+    v[j] = 0ull;
+    if (p < P) {
+      const int64_t item = plan.F + (block - plan.F) * P + p;
+      const uint64_t* kq = gkeys_all + ((size_t)item * k16QB + ql) * C;
+      v[j] = kq[r];
+      if (r == 0) flag |= kq[C - 1] != 0ull;
+    }
+  }
+  wave_sort_desc<E>(v);
+  const int32_t qid = active[qq];
+  int32_t* out = cand + (int64_t)qid * K;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    if (e < K) out[e] = v[j] != 0ull ? key_idx(v[j]) : -1;
+  }
+  if (__ballot(flag) != 0ull && lane == 0) ovf_list[atomicAdd(n_ovf, 1)] = qid;
+}
+
+// Host-side plan: default policy from the device's workgroup slots, or a diagnostic override.
+static int g_plan_rt = -1, g_plan_p = -1;
+static int topk_slots() {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sim_topk_f16<k16Cap, false>, 64 * k16Waves, 0) ==
+            hipSuccess &&
+        cus > 0 && per_cu > 0)
+      slots = cus * per_cu;
+    else
+      slots = 512;  // MI355X: 256 CUs × 2 workgroups
+  }
+  return slots;
+}
+static void host_plan_params(int& rt, int& P) {
+  if (g_plan_rt >= 0 && g_plan_p >= 1) {
+    rt = g_plan_rt;
+    P = g_plan_p;
+    return;
+  }
+  // Whole-table items only, unless the blocks fill at most half of the workgroup slots: then every block is split
+  // into up to 8 pieces to use the idle CUs.  (A/B at cfg2, 1292 blocks on 512 slots: splitting the last 268
+  // blocks into 3 pieces 25.9 ms, the last 512 into 2 26.5 ms, vs 25.5 ms unsplit — a piece restarts the rising
+  // threshold, so P pieces cost ≈ P× the slow path of a block.)
+  rt = 1 << 30;
+  P = 1;
+}
+static void host_plan_for(int64_t max_q, int64_t nd, int& rt, int& P) {
+  host_plan_params(rt, P);
+  if (g_plan_rt < 0) {
+    const int slots = topk_slots();
+    const int64_t nb = cdiv(max_q > 0 ? max_q : 1, k16QB);
+    if (2 * nb <= slots) P = (int)(slots / nb < kMaxPieces ? slots / nb : kMaxPieces);
+  }
+  // every piece streams at least 16 chunks (4,096 domains)
+  const int64_t pmax = cdiv(nd, kChunk) / 16;
+  if (P > pmax) P = (int)(pmax > 1 ? pmax : 1);
+}
+static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
+  int rt, P;
+  host_plan_for(max_q, nd, rt, P);
+  const TopkPlan pl = make_plan(max_q > 0 ? max_q : 1, rt, P);
+  return (size_t)pl.items() * k16QB * k16Cap * sizeof(uint64_t);
 }
 
 template <int C>
@@ -814,19 +978,24 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       set_error("fwav_sim_topk: fp16 search needs its key workspace (fwav_sim_topk_workspace_size)");
       return FWAV_ERR_WORKSPACE;
     }
-    const size_t keys_bytes = f16_keys_bytes(max_q);
+    const size_t keys_bytes = f16_keys_bytes(max_q, nd);
     int32_t* ovf_list = (int32_t*)((char*)gkeys + keys_bytes);
     int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
     (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
     // Geometry: k16Waves waves × k16Sets query sets of 32 per workgroup.  Measured at cfg2 (W, QS=1): W = 8
     // 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms — an even 4 waves per SIMD beats a fuller last round of workgroups.
-    constexpr int NQ = 32 * k16Waves * k16Sets;
-    if (stats != nullptr || (dbg & 255) != 0)
-      k_sim_topk_f16<k16Cap, true><<<cdiv(max_q, NQ), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, dbg & 255, stats);
+    int rt, P;
+    host_plan_for(max_q, nd, rt, P);
+    const TopkPlan pl = make_plan(max_q, rt, P);
+    if (stats != nullptr || (dbg & 8191) != 0)
+      k_sim_topk_f16<k16Cap, true><<<pl.items(), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, dbg & 8191, stats);
     else
-      k_sim_topk_f16<k16Cap, false><<<cdiv(max_q, NQ), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, nullptr);
+      k_sim_topk_f16<k16Cap, false><<<pl.items(), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, 0, nullptr);
+    if (pl.R > 0)
+      k_merge_pieces<k16Cap><<<cdiv(pl.R * k16QB, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, ovf_list,
+                                                                    n_ovf);
     // queries whose fp16 band overflowed the buffer (none for ordinary audio): exact f32 recompute
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32b = false;
@@ -867,7 +1036,7 @@ int fwav_topk_max_k(void) { return 4096; }
 size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   const int64_t q = max_q > 0 ? max_q : 1;
   if (k > 64) return large_workspace_bytes(n_domains, q);
-  return f16_keys_bytes(q) + (size_t)(q + 1) * sizeof(int32_t);
+  return f16_keys_bytes(q, n_domains) + (size_t)(q + 1) * sizeof(int32_t);
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,
@@ -901,6 +1070,15 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t nd, const i
   FWAV_CHECK_ARG(emb && emb16 && workspace && K >= 1 && K <= 64, FWAV_ERR_ARG, "fwav_debug_sim_topk: bad args");
   return launch_topk<128>(emb, (const _Float16*)emb16, nd, active, n_active, max_q, q_offset, K, cand,
                           (hipStream_t)stream, (uint64_t*)workspace, dbg, stats);
+}
+
+// Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
+// fwav_sim_topk_workspace_size after changing it.
+int fwav_debug_topk_plan(int rt, int pieces) {
+  FWAV_CHECK_ARG(pieces >= 1 && pieces <= kMaxPieces, FWAV_ERR_ARG, "fwav_debug_topk_plan: pieces outside [1, 8]");
+  g_plan_rt = rt;
+  g_plan_p = rt < 0 ? -1 : pieces;
+  return FWAV_OK;
 }
 
 }  // extern "C"

@@ -202,3 +202,21 @@ def test_large_k_vs_oracle(K):
     ocand, kth, k1th = orc.topk_candidates(g["emb"], p["n_ranges"], K, pruned)
     same, bad = candidate_agreement(cand, ocand, kth, k1th, g["emb"][:len(cand)], pruned)
     assert not bad.any(), f"K={K}: {bad.sum()} unexplained mismatches"
+
+
+@pytest.mark.parametrize("plan", [(0, 1), (1 << 20, 2), (1 << 20, 5), (1 << 20, 8), (10, 3)])
+def test_f16_split_plans_equal_f32(plan):
+    """Work plans that split query blocks into table pieces (merged by k_merge_pieces) return exactly the
+    unsplit search's candidates: whole, all blocks in 2/5/8 pieces, and only the last 10 blocks in 3."""
+    from fwav import synth
+    sig = synth.noise(6.0, 44100, seed=11)
+    b, _ = _cands(sig, 2048, 64, "f32")
+    call("fwav_debug_topk_plan", *plan)
+    try:
+        a, _ = _cands(sig, 2048, 64, "f16")
+        p, _ = _cands(_periodic(), 1024, 32, "f16")  # band overflow inside pieces → f32 recompute after the merge
+    finally:
+        call("fwav_debug_topk_plan", -1, 1)
+    assert np.array_equal(a, b)
+    q, _ = _cands(_periodic(), 1024, 32, "f32")
+    assert np.array_equal(p, q)

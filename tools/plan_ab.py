@@ -1,0 +1,61 @@
+"""A/B the fp16 search's work plan (fwav_debug_topk_plan) in one process on the cfg2 inputs; outputs must be
+identical to the unsplit plan.  usage: python tools/plan_ab.py "0:1,512:2,512:3" [seconds]"""
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd")]
+import numpy as np
+import torch
+
+import __graft_entry__
+
+__graft_entry__.build()
+from fwav import engine, synth  # noqa: E402
+from fwav._lib import call, size_call  # noqa: E402
+
+plans = [tuple(int(x) for x in p.split(":")) for p in sys.argv[1].split(",")]
+secs = float(sys.argv[2]) if len(sys.argv) > 2 else 60.0
+sig = torch.from_numpy(synth.noise(secs, 44100)).cuda()
+r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
+torch.cuda.synchronize()
+nd, nr = r.n_domains, r.n_ranges
+emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+tab = engine.embed_tables(8, torch.device("cuda"))
+pool = torch.empty(nd * 8, device="cuda")
+emb = torch.empty(nd * 16, device="cuda")
+ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
+     emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+nq = int(os.environ.get("AB_NQ", nr))
+active = torch.arange(nq, dtype=torch.int32, device="cuda")
+n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
+ref = None
+res = []
+for rnd in range(3):
+    for rt, P in plans:
+        call("fwav_debug_topk_plan", rt, P)
+        wsn = size_call("fwav_sim_topk_workspace_size", nq, nd, 64)
+        wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
+        cand = torch.empty(nq * 64, dtype=torch.int32, device="cuda")
+        ts = []
+        for _ in range(3):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            call("fwav_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
+                 64, cand.data_ptr(), wsk.data_ptr(), wsn, st)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        if ref is None:
+            ref = cand.clone()
+        same = bool(torch.equal(cand, ref))
+        if rnd == 2:
+            res.append((rt, P, np.median(ts), min(ts), same, wsn))
+        del wsk
+call("fwav_debug_topk_plan", -1, 1)
+for rt, P, med, mn, same, wsn in res:
+    print(f"plan rt={rt:5d} P={P}: median {med:7.2f} ms  min {mn:7.2f}  identical={same}  workspace {wsn / 2**30:.2f} GiB",
+          flush=True)

@@ -1,7 +1,8 @@
 """Time the similarity search kernel with diagnostic ablations (tools only; outputs are wrong for dbg & 7 != 0).
 
 dbg bits (k_sim_topk_f16, STATS build): 1 = no slow path, 2 = skip MFMA + filter, 4 = no chunk DMA beyond one
-chunk, 128 = DMA every other chunk (geometry variants: tools/ab_build.sh + tools/ab_topk.py).
+chunk, 128 = DMA every other chunk, 256 = no group barrier, 512 = fold without ballots, 1024 = MFMA without fold.
+usage: python tools/topk_ablate.py [seconds] [dbg,dbg,...] (geometry variants: tools/ab_build.sh + tools/ab_topk.py).
 Counters: replayed chunks, firing tiles, appends, compactions, per-segment tick shares, overflow fallbacks."""
 import os, sys, time
 sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -59,7 +60,7 @@ for dbg in (1, 4):
           "streaming %.3f, replays %.3f, final %.3f, other %.3f" %
           (dbg, sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr, sv[7] / tot, sv[9] / tot, sv[4] / tot,
            sv[8] / tot, 1 - (sv[7] + sv[9] + sv[4] + sv[8]) / tot), flush=True)
-for dbg in [0, 1, 4, 5, 128, 2, 0]:
+for dbg in ([int(x) for x in sys.argv[2].split(',')] if len(sys.argv) > 2 else [0, 1, 4, 5, 128, 2, 0]):
     for rep in range(2):
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
