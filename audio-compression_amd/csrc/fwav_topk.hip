@@ -250,6 +250,23 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 // array out of registers).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr float kF16Delta = 2.5e-3f;
+#ifdef FWAV_TOPK_DEBUG
+// Debug builds only (tools/ab_build.sh … -DFWAV_TOPK_DEBUG=<query>): seeds of every query and an event trace of one.
+__device__ uint32_t g_fwav_dbg[(1 << 20) + (1 << 16)];
+__device__ uint32_t g_fwav_dbg_n;
+#define FWAV_TRACE(qid, a, b, c, d)                                                         \
+  do {                                                                                    \
+    if ((qid) == FWAV_TOPK_DEBUG) {                                                       \
+      const uint32_t i_ = atomicAdd(&g_fwav_dbg_n, 1u);                                   \
+      if (i_ < (1 << 14)) {                                                               \
+        g_fwav_dbg[(1 << 20) + 4 * i_] = (a); g_fwav_dbg[(1 << 20) + 4 * i_ + 1] = (b);    \
+        g_fwav_dbg[(1 << 20) + 4 * i_ + 2] = (c); g_fwav_dbg[(1 << 20) + 4 * i_ + 3] = (d); \
+      }                                                                                   \
+    }                                                                                     \
+  } while (0)
+#else
+#define FWAV_TRACE(qid, a, b, c, d) do { } while (0)
+#endif
 
 // Diagnostic counters (fwav_debug_sim_topk only; stays nullptr in production launches), summed over waves:
 //   [0] replayed chunks  [1] firing tiles  [2] appends  [3] streaming compactions
@@ -366,6 +383,12 @@ struct Topk16SmemT {
 // finds T ≤ key(S16) with ballots and scalar popcounts (≈ 80 VALU ops, vs ≈ 1,300 + 264 LDS shuffles for a
 // 256-key bitonic sort).  If the band would not leave 64 free slots the query is flagged (ovf) and later
 // recomputed by the exact f32 kernel.
+// Key-buffer reads: L2-served (sc1), never a possibly stale L1 copy of a line this wave loaded before its later
+// appends to it.
+__device__ __forceinline__ uint64_t ld_key(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int C, class SM>
 __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n_in, SM& sm, int ql, int K,
                                               unsigned long long* stats, int& m_out, float& lim_out) {
@@ -379,7 +402,7 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n_i
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
-    v[j] = e < n ? kq[e] : 0ull;
+    v[j] = e < n ? ld_key(kq + e) : 0ull;
     hi[j] = (uint32_t)(v[j] >> 32);  // 0 for empty slots; f2key of any real score is > 0
   }
   float lim = -INFINITY;
@@ -410,6 +433,7 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n_i
     ovf = 1;
   }
   if (lane == 0 && ovf) sm.ovf[ql] = 1;
+  if (lane == 0) FWAV_TRACE(sm.qrow[ql], 2u, (uint32_t)n, __float_as_uint(lim), (uint32_t)((ovf << 16) | m));
   m_out = m;
   lim_out = lim;
   if (stats) {
@@ -434,7 +458,7 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
-    v[j] = e < n ? kq[e] : 0ull;
+    v[j] = e < n ? ld_key(kq + e) : 0ull;
   }
   float qv[16];
 #pragma unroll
@@ -528,6 +552,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
   // the query's count lives in a register of both its lanes (h = 0, 1): no LDS atomic, no LDS read-back
   const int cntm = __builtin_popcount(mask);
   const int other = __shfl_xor(cntm, 32);
+  FWAV_TRACE(sm.qrow[ql], 1u, (uint32_t)dt, (uint32_t)((h << 16) | mask), (uint32_t)qcnt);
   const int base_i = qcnt + (h ? other : 0);
   qcnt += cntm + other;  // ≤ C: compaction below keeps qcnt ≤ C − 32 before a tile adds ≤ 32
   // static slots: slot r's key goes to base + popcount of the lower set bits (exec-masked store); faster than a
@@ -551,7 +576,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
                      STATS ? stats : nullptr, m, lim);
     if (col == l) {
       qcnt = m;
-      if (upd) thf = lim;
+      if (upd) thf = fmaxf(thf, lim);  // the seed may be above a buffer's own limit
     }
   }
   return thf;
@@ -612,6 +637,62 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
     if (ct[kReplayBatch - 1] < 0) break;
   }
   return thf;
+}
+
+// Seed of a query's band limit before the stream: the K-th largest s16 among the domains of its own window
+// [qrow − 64, qrow + 64).  Consecutive domains are windows 2 samples apart, so this window holds close matches and
+// its K-th score is far above what the first streamed chunks give; a valid start for the rising limit (K domains
+// have s16 ≥ T, so every exact top-K member has s16 > T − 2δ), it removes the first compactions and ≈ 1/4 of the
+// appends.  The wave's window tiles (6 × 32 domains from a tile-aligned base, read from L2/MALL) are scored with
+// the stream's own MFMA, recomputed per radix step (a greedy bitwise select over the non-negative keys, ballots
+// free: each query's two lanes combine their counts by one shuffle).  Returns −∞ when fewer than K window scores
+// are ≥ 0.
+constexpr int kSeedTiles = 6;
+constexpr int kSeedHalf = 64;
+__device__ __forceinline__ float seed_limit(const _Float16* __restrict__ emb16, int64_t nd, half8 b, int64_t qrow,
+                                            int64_t wbase, int K) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 31;
+  const int h = lane >> 5;
+  const half8* afp[kSeedTiles];
+  uint32_t wm[kSeedTiles];  // per tile: the lane's 16 outputs that are in its query's window (and the table)
+#pragma unroll
+  for (int t = 0; t < kSeedTiles; ++t) {
+    const int64_t dt = wbase + 32 * t;
+    const bool ok = dt >= 0 && dt < nd;
+    const int64_t c = ok ? dt / kChunk : 0, tt = ok ? (dt % kChunk) / 32 : 0;
+    afp[t] = reinterpret_cast<const half8*>(emb16 + ((c * 2 + h) * kChunk + col) * 8 + tt * 256);
+    uint32_t m = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t d = dt + 4 * h + (r & 3) + 8 * (r >> 2);
+      m |= (ok && d < nd && d >= qrow - kSeedHalf && d < qrow + kSeedHalf) ? (1u << r) : 0u;
+    }
+    wm[t] = m;
+  }
+  auto count_ge = [&](float thr) {
+    int c = 0;
+    half8 af[kSeedTiles];  // re-read per step (L2): keeps the prologue's register peak below the stream's
+#pragma unroll
+    for (int t = 0; t < kSeedTiles; ++t) af[t] = *afp[t];
+#pragma unroll
+    for (int t = 0; t < kSeedTiles; ++t) {
+      const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[t], b, floatx16{}, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) c += ((wm[t] >> r) & 1u) && acc[r] >= thr ? 1 : 0;
+    }
+    return c + __shfl_xor(c, 32);
+  };
+  // No per-lane branches here: the MFMAs and shuffles need the whole wave active (a per-lane early return let the
+  // compiler run the select loop under a partial EXEC, which corrupts both)
+  const bool ok = count_ge(0.0f) >= K;
+  uint32_t T = 0x80000000u;  // key of +0.0
+  for (int bit = 30; bit >= 12; --bit) {
+    const uint32_t Tc = T | (1u << bit);
+    const int c = count_ge(key2f(Tc));
+    T = c >= K ? Tc : T;
+  }
+  return ok ? key2f(T) - 2.0f * kF16Delta : -INFINITY;
 }
 
 // NC chunks from the LDS slots as a single unrolled software pipeline over their 8·NC tiles: fragments are read
@@ -719,7 +800,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
   // dbg (STATS builds only; timing ablations, outputs invalid): 1 = never take the slow path,
   // 2 = skip MFMA + threshold test, 4 = no global chunk loads, 128 = DMA only every other chunk,
   // 256 = no group barrier, 512 = fold without ballots, 1024 = MFMA without fold, 4096 = record the workgroup
-  // timeline (combinable with the others)
+  // timeline (combinable with the others), 8192 = no seeded band limits
   if (!STATS) dbg = 0;
   half8 b[QS];
   float thf[QS];
@@ -739,6 +820,23 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     }
   }
 
+  // seed the band limits from the queries' own domain windows (tiles from the wave's first query row)
+  if (!(STATS && (dbg & 8192))) {  // ablation 8192: no seed
+#pragma unroll
+    for (int s = 0; s < QS; ++s) {
+      // whole wave (MFMA + shuffles); lanes of unused query slots discard the result
+      const int64_t wbase =
+          (int64_t)((__builtin_amdgcn_readfirstlane((int)sm.qrow[(wave * QS + s) * 32]) - kSeedHalf) >> 5) << 5;
+      const float seed = seed_limit(emb16, nd, b[s], sm.qrow[(wave * QS + s) * 32 + col], wbase, K);
+      if (upd[s]) thf[s] = seed;
+#ifdef FWAV_TOPK_DEBUG
+      if (upd[s] && sm.qrow[(wave * QS + s) * 32 + col] < (1 << 19))
+        g_fwav_dbg[sm.qrow[(wave * QS + s) * 32 + col] + (h << 19)] = __float_as_uint(seed);
+#endif
+      if (STATS && (dbg & 32768) && gstats != nullptr && h == 0 && upd[s])  // diagnostics: the seeds
+        gstats[16 + qbase + (wave * QS + s) * 32 + col] = __float_as_uint(seed);
+    }
+  }
   const int64_t nchunks = cdiv(nd, kChunk);
   // this item's chunk range [c0, c1) (the whole table unless the block is split)
   const int64_t c0 = nchunks * piece / npieces, c1 = nchunks * (piece + 1) / npieces;
@@ -842,6 +940,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     if (qq >= n_active) break;
     const int32_t qid = active[qq];
     uint64_t* kq = gkeys + (size_t)qs * C;
+    if (lane == 0) FWAV_TRACE(sm.qrow[qs], 3u, (uint32_t)sm.cnt[qs], (uint32_t)sm.ovf[qs], 0u);
     compact16<C>(kq, sm, qs, K, emb, STATS ? stats : nullptr);  // exact f32 rescoring of the kept band + sort
     const int n = sm.cnt[qs];
     if (npieces == 1) {
@@ -987,9 +1086,9 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     int rt, P;
     host_plan_for(max_q, nd, rt, P);
     const TopkPlan pl = make_plan(max_q, rt, P);
-    if (stats != nullptr || (dbg & 8191) != 0)
+    if (stats != nullptr || (dbg & 65535) != 0)
       k_sim_topk_f16<k16Cap, true><<<pl.items(), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, dbg & 8191, stats);
+          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, dbg & 65535, stats);
     else
       k_sim_topk_f16<k16Cap, false><<<pl.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, 0, nullptr);
@@ -1072,6 +1171,14 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t nd, const i
                           (hipStream_t)stream, (uint64_t*)workspace, dbg, stats);
 }
 
+#ifdef FWAV_TOPK_DEBUG
+int fwav_debug_dump(void* host, size_t bytes, unsigned* n_events) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwav_dbg), bytes);
+  (void)hipMemcpyFromSymbol(n_events, HIP_SYMBOL(g_fwav_dbg_n), sizeof(unsigned));
+  return FWAV_OK;
+}
+#endif
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.
 int fwav_debug_topk_plan(int rt, int pieces) {

@@ -1,0 +1,81 @@
+"""Event trace of one query in a -DFWAV_TOPK_DEBUG=<q> build (tools/ab_build.sh): seeds, appends, compactions.
+usage: python tools/diag_trace.py tools/ab/libfwav_dbgQ.so case K Q"""
+import ctypes as C
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd"),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests")]
+import numpy as np
+import torch
+
+import __graft_entry__
+
+__graft_entry__.build()
+from fwav import engine  # noqa: E402
+from fwav._lib import SIGNATURES, call, size_call  # noqa: E402
+from golden_util import load  # noqa: E402
+from oracle import fractal_oracle as O  # noqa: E402
+
+L = C.CDLL(os.path.abspath(sys.argv[1]))
+for n in ("fwav_sim_topk", "fwav_debug_topk_plan", "fwav_sim_topk_workspace_size", "fwav_pool_embed",
+          "fwav_pool_workspace_size"):
+    getattr(L, n).restype, getattr(L, n).argtypes = SIGNATURES[n]
+case, K, Q = sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+g = load(case)
+p = g["p"]
+sig = torch.from_numpy(g["signal"]).cuda()
+r = engine.compress_device(sig, p["tile"], K, energy_thresh=p["thr"], keep_intermediates=True, search="f32")
+torch.cuda.synchronize()
+ref = r.cand.cpu().numpy().reshape(-1, K)
+nd, nr = r.n_domains, r.n_ranges
+rs, step = O.geometry(p["tile"])[:2]
+emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+tab = engine.embed_tables(rs, torch.device("cuda"))
+pool = torch.empty(nd * rs, device="cuda")
+emb = torch.empty(nd * 16, device="cuda")
+ws = torch.empty(L.fwav_pool_workspace_size(sig.numel(), p["tile"], rs, step), dtype=torch.uint8, device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+assert L.fwav_pool_embed(sig.data_ptr(), sig.numel(), p["tile"], rs, step, tab.data_ptr(), pool.data_ptr(),
+                         emb.data_ptr(), emb16.data_ptr(), ws.data_ptr(), ws.numel(), st) == 0
+active = torch.arange(nr, dtype=torch.int32, device="cuda")
+n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
+L.fwav_debug_topk_plan(0, 1)
+wsn = L.fwav_sim_topk_workspace_size(nr, nd, K)
+wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
+cand = torch.full((nr * K,), -7, dtype=torch.int32, device="cuda")
+assert L.fwav_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0, K,
+                       cand.data_ptr(), wsk.data_ptr(), wsn, st) == 0
+torch.cuda.synchronize()
+c = cand.cpu().numpy().reshape(-1, K)
+print("rows differing from f32:", np.nonzero(~np.all(c == ref, axis=1))[0][:20])
+buf = np.zeros((1 << 20) + (1 << 16), dtype=np.uint32)
+ne = C.c_uint(0)
+L.fwav_debug_dump.restype = C.c_int
+L.fwav_debug_dump(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes), C.byref(ne))
+E = emb.cpu().numpy().reshape(-1, 16).astype(np.float64)
+E16 = emb16.cpu().numpy().astype(np.float64)
+s = E @ E[Q]
+order = np.argsort(-s, kind="stable")
+print(f"q {Q}: seed h0 {buf[Q:Q + 1].view(np.float32)[0]:.6f} h1 {buf[Q + (1 << 19):Q + (1 << 19) + 1].view(np.float32)[0]:.6f}, true kth {s[order[K - 1]]:.6f}, events {ne.value}")
+print("missing:", sorted(set(ref[Q]) - set(c[Q])), "extra:", sorted(set(c[Q]) - set(ref[Q])))
+ev = buf[1 << 20:(1 << 20) + 4 * min(ne.value, 1 << 14)].reshape(-1, 4)
+appended = set()
+sd0 = buf[:nr].view(np.float32)
+sd1 = buf[1 << 19:(1 << 19) + nr].view(np.float32)
+dif = np.nonzero(sd0 != sd1)[0]
+print("queries whose two lanes got different seeds:", len(dif), dif[:20], sd0[dif[:5]], sd1[dif[:5]])
+for t, a, b, d in ev:
+    if t == 1:
+        dt, h, mask, qcnt = int(a), int(b >> 16), int(b & 0xffff), int(d)
+        doms = [dt + 4 * h + (rr & 3) + 8 * (rr >> 2) for rr in range(16) if mask >> rr & 1]
+        appended.update(doms)
+        print(f"  append dt={dt} h={h} qcnt={qcnt} n={len(doms)} doms={doms[:6]}{'...' if len(doms) > 6 else ''}")
+    elif t == 2:
+        print(f"  compact n={a} lim={np.uint32(b).view(np.float32):.6f} m={d & 0xffff} ovf={d >> 16}")
+    elif t == 3:
+        print(f"  final cnt={a} ovf={b}")
+miss = sorted(set(ref[Q]) - set(c[Q]))
+print("missing domains ever appended:", [m for m in miss if m in appended])
+L.fwav_debug_topk_plan(-1, 1)

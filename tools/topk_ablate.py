@@ -53,8 +53,7 @@ for dbg in (1, 4):
     torch.cuda.synchronize()
     sv = stats.cpu().tolist()
     tot = sv[6]
-    keys_bytes = (-(-nr // 32) * 32 + 512) * 256 * 8
-    n_ovf = int(wsk[keys_bytes + 4 * nr: keys_bytes + 4 * nr + 4].view(torch.int32).item())
+    n_ovf = int(wsk[wsk.numel() - 4:].view(torch.int32).item())  # workspace tail: ovf list, then its count
     print("dbg=%d: overflowed queries (f32 recompute) %d" % (dbg, n_ovf))
     print("dbg=%d: replays/wave %.0f firing tiles/wave %.0f appends/q %.0f compactions/q %.2f | shares: barrier %.3f, "
           "streaming %.3f, replays %.3f, final %.3f, other %.3f" %
