@@ -1015,40 +1015,50 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
 
 // Host-side plan: default policy from the device's workgroup slots, or a diagnostic override.
 static int g_plan_rt = -1, g_plan_p = -1;
-static int topk_slots() {
-  static int slots = 0;
-  if (slots == 0) {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sim_topk_f16<k16Cap, false>, 64 * k16Waves, 0) ==
-            hipSuccess &&
-        cus > 0 && per_cu > 0)
-      slots = cus * per_cu;
-    else
-      slots = 512;  // MI355X: 256 CUs × 2 workgroups
+static void topk_device_slots(int& cus, int& per_cu) {
+  static int c = 0, w = 0;
+  if (c == 0) {
+    int dev = 0;
+    if (!(hipGetDevice(&dev) == hipSuccess &&
+          hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false>, 64 * k16Waves, 0) ==
+              hipSuccess &&
+          c > 0 && w > 0)) {
+      c = 256;  // MI355X: 256 CUs × 2 workgroups
+      w = 2;
+    }
   }
-  return slots;
+  cus = c;
+  per_cu = w;
 }
-static void host_plan_params(int& rt, int& P) {
+// Default policy.  Whole-table items, dispatched in order, fill the slots round after round; the last round's
+// workgroups run faster when they have a CU to themselves, but once that round holds more blocks than there are
+// CUs, the surplus doubles up on a few CUs and finishes last (cfg2: 1292 blocks on 256 CUs × 2 → the last 268 blocks
+// include 12 that ran 3.5 ms past the rest).  So the last 2·(surplus) blocks are split into 4 table pieces, which
+// fill in beside the lone workgroups (cfg2 A/B: 24.9 → 22.6 ms; splitting more blocks costs more than it saves,
+// since every piece restarts the rising limit: 268 blocks in 2 pieces 24.2 ms, 512 in 2 25.3 ms).  Few blocks
+// (at most half the slots) are each split into up to 8 pieces so that the table passes use the idle CUs.
+static void host_plan_for(int64_t max_q, int64_t nd, int& rt, int& P) {
   if (g_plan_rt >= 0 && g_plan_p >= 1) {
     rt = g_plan_rt;
     P = g_plan_p;
-    return;
-  }
-  // Whole-table items only, unless the blocks fill at most half of the workgroup slots: then every block is split
-  // into up to 8 pieces to use the idle CUs.  (A/B at cfg2, 1292 blocks on 512 slots: splitting the last 268
-  // blocks into 3 pieces 25.9 ms, the last 512 into 2 26.5 ms, vs 25.5 ms unsplit — a piece restarts the rising
-  // threshold, so P pieces cost ≈ P× the slow path of a block.)
-  rt = 1 << 30;
-  P = 1;
-}
-static void host_plan_for(int64_t max_q, int64_t nd, int& rt, int& P) {
-  host_plan_params(rt, P);
-  if (g_plan_rt < 0) {
-    const int slots = topk_slots();
+  } else {
+    int cus, per_cu;
+    topk_device_slots(cus, per_cu);
+    const int64_t slots = (int64_t)cus * per_cu;
     const int64_t nb = cdiv(max_q > 0 ? max_q : 1, k16QB);
-    if (2 * nb <= slots) P = (int)(slots / nb < kMaxPieces ? slots / nb : kMaxPieces);
+    rt = 0;
+    P = 1;
+    if (2 * nb <= slots) {
+      rt = (int)nb;
+      P = (int)(slots / nb < kMaxPieces ? slots / nb : kMaxPieces);
+    } else {
+      const int64_t last = nb % slots == 0 ? slots : nb % slots;  // blocks in the last round
+      if (last > cus) {
+        rt = (int)(2 * (last - cus) < nb ? 2 * (last - cus) : nb);
+        P = 4;
+      }
+    }
   }
   // every piece streams at least 16 chunks (4,096 domains)
   const int64_t pmax = cdiv(nd, kChunk) / 16;
