@@ -291,6 +291,19 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_QS
 #define FWAV_TOPK_QS 1
 #endif
+#ifndef FWAV_TOPK_WPE
+#define FWAV_TOPK_WPE 4  // launch bound: waves per SIMD the register allocation must allow
+#endif
+// Ablation builds (tools/ab_build.sh NAME -DFWAV_TOPK_ABL=<dbg bits>): the production kernel with the given `dbg`
+// bits fixed at compile time — the STATS kernel's counters cost registers (it spills), which skews its timings.
+#ifndef FWAV_TOPK_ABL
+#define FWAV_TOPK_ABL 0
+#endif
+// STAGGER: the second half of the waves takes each group's chunks in rotated order (A/B at cfg2: 22.85 → 22.46 ms;
+// a static s_setprio for that half instead was slower, 23.50 ms)
+#ifndef FWAV_TOPK_STAGGER
+#define FWAV_TOPK_STAGGER 1
+#endif
 constexpr int kGroup = FWAV_TOPK_G;     // chunks per barrier
 constexpr int k16Waves = FWAV_TOPK_W;   // waves per workgroup
 constexpr int k16Sets = FWAV_TOPK_QS;   // query sets of 32 per wave (each LDS fragment feeds k16Sets MFMAs)
@@ -327,8 +340,14 @@ __host__ __device__ inline void plan_item(const TopkPlan& pl, int64_t item, int6
     block = pl.F + j / pl.P; piece = (int)(j % pl.P); np = pl.P;
   }
 }
-constexpr int kWindowGroups = 16;    // after the warm-up, fired chunks are replayed every 16 groups (64 chunks)
-constexpr int kWarmChunks = 64;      // ... and after every group during the first 64 chunks
+#ifndef FWAV_TOPK_WIN
+#define FWAV_TOPK_WIN 16
+#endif
+#ifndef FWAV_TOPK_WARM
+#define FWAV_TOPK_WARM 64
+#endif
+constexpr int kWindowGroups = FWAV_TOPK_WIN;  // after the warm-up, fired chunks are replayed every 16 groups (64 chunks)
+constexpr int kWarmChunks = FWAV_TOPK_WARM;   // ... and after every group during the first 64 chunks
 
 
 __device__ __forceinline__ float score32(const float* __restrict__ emb, int64_t d, const float (&q)[16]) {
@@ -369,7 +388,8 @@ __device__ __forceinline__ bool may_pass(int imx, float thf) {
 // slots + this) must fit one CU's 160 KB of LDS.
 template <int NG, bool STATS>
 struct Topk16SmemT {
-  int cnt[32 * NG];  // final pass: entries in the query's buffer
+  int cnt[32 * NG];   // final pass: entries at the front of the query's buffer (its h = 0 lane's appends)
+  int cnt1[32 * NG];  // ... and at the back (its h = 1 lane's)
   int ovf[32 * NG];  // band overflowed the buffer: recompute this query with the f32 kernel
   int64_t qrow[32 * NG];
   uint32_t fired[NG][kWindowGroups * 4];           // per-group deferred work: chunk indices of a window
@@ -389,20 +409,26 @@ __device__ __forceinline__ uint64_t ld_key(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Entry e of a two-ended buffer holding n0 entries at the front and n1 at the back (append_tile).
+template <int C>
+__device__ __forceinline__ int two_end_slot(int e, int n0) {
+  return e < n0 ? e : C - 1 - (e - n0);
+}
+
 template <int C, class SM>
-__device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n_in, SM& sm, int ql, int K,
+__device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0, int n1, SM& sm, int ql, int K,
                                               unsigned long long* stats, int& m_out, float& lim_out) {
   constexpr int E = C / 64;
   const unsigned long long t_start = stats ? __builtin_amdgcn_s_memrealtime() : 0;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int n = min(n_in, C);
+  const int n = min(n0 + n1, C);
   uint64_t v[E];
   uint32_t hi[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
-    v[j] = e < n ? ld_key(kq + e) : 0ull;
+    v[j] = e < n ? ld_key(kq + two_end_slot<C>(e, n0)) : 0ull;
     hi[j] = (uint32_t)(v[j] >> 32);  // 0 for empty slots; f2key of any real score is > 0
   }
   float lim = -INFINITY;
@@ -442,23 +468,24 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n_i
   }
 }
 
-// Final pass of query ql: rescore its buffer kq[0 .. cnt) in exact f32, sort, keep the top K.  Whole wave.
-// Every per-query buffer and counter is owned by one wave, so no cross-wave fences are needed; the wave's
-// own appended stores are drained once (vmcnt(0)), then all key loads and all row loads are issued
-// together (two memory round trips in total).
+// Final pass of query ql: rescore its two-ended buffer (sm.cnt entries at the front, sm.cnt1 at the back) in exact
+// f32, sort, emit the top K (to `out`, or for a piece back into kq).  Whole wave.  Every per-query buffer and
+// counter is owned by one wave, so no cross-wave fences are needed; the wave's own appended stores are drained
+// once (vmcnt(0)), then all key loads and all row loads are issued together (two memory round trips in total).
 template <int C, class SM>
 __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
-                                          const float* __restrict__ emb, unsigned long long* stats) {
+                                          const float* __restrict__ emb, int32_t* __restrict__ out) {
   constexpr int E = C / 64;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int n = min(sm.cnt[ql], C);
+  const int n0 = sm.cnt[ql];
+  const int n = min(n0 + sm.cnt1[ql], C);
   const float4* qp = reinterpret_cast<const float4*>(emb + sm.qrow[ql] * 16);
   uint64_t v[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
-    v[j] = e < n ? ld_key(kq + e) : 0ull;
+    v[j] = e < n ? ld_key(kq + two_end_slot<C>(e, n0)) : 0ull;
   }
   float qv[16];
 #pragma unroll
@@ -498,12 +525,19 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
     }
   }
   wave_sort_desc<E>(v);
+  // Emit straight from registers (never read back what was just stored: a load issued right behind the stores
+  // of the same addresses can return the old contents).  A whole-table item writes the K candidate indices,
+  // −1-padded; a piece leaves its sorted exact top K in the buffer, 0-padded, for k_merge_pieces.
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
-    if (e < K && e < n) kq[e] = v[j];
+    if (e < K) {
+      if (out != nullptr)
+        out[e] = e < n ? key_idx(v[j]) : -1;
+      else
+        kq[e] = e < n ? v[j] : 0ull;
+    }
   }
-  if (lane == 0) sm.cnt[ql] = n < K ? n : K;
 }
 
 // Integer filter threshold for the fold-max test: (int)x > thi ⟺ x > thf for non-NaN x when thf >= 0;
@@ -538,44 +572,53 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
   const int ql = qg * 32 + col;  // qg: the wave-uniform query group (32 queries) of this tile
   if (__ballot(fold16((int)0x80000000, acc) > int_threshold(thf)) == 0ull) return thf;
   if (STATS) stat_add(1, 1);
-  uint64_t* kq = gkeys + (size_t)ql * C;
-  const int64_t d0 = dt + 4 * h;
-  uint32_t mask = 0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) mask |= acc[r] > thf ? (1u << r) : 0u;
-  if (dt + 32 > nd) {
+  const unsigned long long t_a0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+  // Two-ended buffer: the h = 0 lane of a query appends at the front (slots 0, 1, …), the h = 1 lane at the back
+  // (C−1, C−2, …), so a lane stores each survivor at its own running slot as soon as its compare passes: one
+  // compare, the key and one exec-masked store per row, and no per-tile exchange of counts before the stores.
+  // Byte offsets from the item's key region stay 32-bit (≤ 32·NG·C·8 B).
+  const uint32_t nd0 = ~(uint32_t)(dt + 4 * h);  // key low word of row r: ~(domain index) = nd0 − offset(r)
+  floatx16 a = acc;
+  if (dt + 32 > nd) {  // wave-uniform: the table's last tile; rows past the end never pass
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      if (d0 + (r & 3) + 8 * (r >> 2) >= nd) mask &= ~(1u << r);
+      if (dt + 4 * h + (r & 3) + 8 * (r >> 2) >= nd) a[r] = -INFINITY;
   }
-  const unsigned long long t_a0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-  // the query's count lives in a register of both its lanes (h = 0, 1): no LDS atomic, no LDS read-back
-  const int cntm = __builtin_popcount(mask);
-  const int other = __shfl_xor(cntm, 32);
-  FWAV_TRACE(sm.qrow[ql], 1u, (uint32_t)dt, (uint32_t)((h << 16) | mask), (uint32_t)qcnt);
-  const int base_i = qcnt + (h ? other : 0);
-  qcnt += cntm + other;  // ≤ C: compaction below keeps qcnt ≤ C − 32 before a tile adds ≤ 32
-  // static slots: slot r's key goes to base + popcount of the lower set bits (exec-masked store); faster than a
-  // per-lane ctz loop, whose acc[r] with a per-lane r is a 16-way v_cndmask chain per append
+  const int before = qcnt;
+  int slot = h ? C - 1 - qcnt : qcnt;
+  const int step = h ? -1 : 1;
+  char* kbase = reinterpret_cast<char*>(gkeys);
 #pragma unroll
-  for (int r = 0; r < 16; ++r)
-    if (mask & (1u << r))
-      kq[base_i + __builtin_popcount(mask & ((1u << r) - 1u))] =
-          make_key(acc[r], (int32_t)(d0 + (r & 3) + 8 * (r >> 2)));
+  for (int r = 0; r < 16; ++r) {
+    if (a[r] > thf) {
+      FWAV_TRACE(sm.qrow[ql], 1u, (uint32_t)dt, (uint32_t)((h << 16) | r), (uint32_t)slot);
+      // f2key, branch-free: negative → ~u, else u | sign
+      const uint32_t u = __float_as_uint(a[r]);
+      const uint32_t key = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+      *reinterpret_cast<uint64_t*>(kbase + (uint32_t)((ql * C + slot) * 8)) =
+          ((uint64_t)key << 32) | (uint64_t)(nd0 - (uint32_t)((r & 3) + 8 * (r >> 2)));
+      slot += step;
+    }
+  }
+  qcnt = h ? C - 1 - slot : slot;  // this lane's entries; ≤ C in total: see the compaction trigger below
+  // the query's total (both lanes) in every lane, by one cross-half swap
+  const auto sw = __builtin_amdgcn_permlane32_swap((uint32_t)qcnt, (uint32_t)qcnt, false, false);
+  const int total = (int)(sw[0] + sw[1]);
   if (STATS) {
-    stat_add(2, __ockl_wfred_add_u32((uint32_t)cntm));
+    stat_add(2, __ockl_wfred_add_u32((uint32_t)(qcnt - before)));
     stat_add(10, __builtin_amdgcn_s_memrealtime() - t_a0);
   }
-  uint64_t need = __ballot(lane < 32 && qcnt > C - 32);
+  // compact when fewer than 32 free slots remain (a tile adds ≤ 16 per lane, ≤ 32 per query)
+  uint64_t need = __ballot(lane < 32 && total > C - 32);
   while (need != 0ull) {
     const int l = __builtin_ctzll(need);
     need &= need - 1;
     int m;
     float lim;
-    compact16_s16<C>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l), sm, qg * 32 + l, K,
-                     STATS ? stats : nullptr, m, lim);
+    compact16_s16<C>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l),
+                     __builtin_amdgcn_readlane(qcnt, l + 32), sm, qg * 32 + l, K, STATS ? stats : nullptr, m, lim);
     if (col == l) {
-      qcnt = m;
+      qcnt = h ? 0 : m;  // the kept band is written densely at the front
       if (upd) thf = fmaxf(thf, lim);  // the seed may be above a buffer's own limit
     }
   }
@@ -703,14 +746,17 @@ __device__ __forceinline__ float seed_limit(const _Float16* __restrict__ emb16, 
 // recorded in its set's row as (chunk << 4 | chain mask).
 // MODE (timing ablations, STATS builds only): 1 = fold but no ballots/records, 2 = MFMA with a 2-output fold
 // (one v_max3 per tile instead of 8; results kept alive through `sink`).
-template <int NC, int QS, int MODE = 0>
+// ROT: the group's chunks are taken in rotated order (chunk (k + ROT) mod NC at step k) — a stagger between the
+// two halves of the workgroup, which otherwise reach their MFMA and fold phases in lockstep.
+template <int NC, int QS, int MODE = 0, int ROT = 0>
 __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, const half8 (&b)[QS],
                                              const int (&thi)[QS], int64_t cbase, uint32_t (*fired)[kWindowGroups * 4],
                                              int (&nfired)[QS], int lane, int* sink = nullptr) {
   constexpr int NT = 8 * NC;
   constexpr int kChunkHalfs = 512 * 8;  // one 8 KB chunk slot
+  auto chunk_of = [](int i) { return ((i >> 3) + ROT) % NC; };
   auto rd = [&](int i) {
-    return *reinterpret_cast<const half8*>(lda0 + (i >> 3) * kChunkHalfs + (i & 7) * 256);
+    return *reinterpret_cast<const half8*>(lda0 + chunk_of(i) * kChunkHalfs + (i & 7) * 256);
   };
   half8 a[NT];
   floatx16 acc[NT][QS];
@@ -746,7 +792,7 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
         const uint32_t m4 = (__ballot(r[s][0] > t) != 0ull ? 1u : 0u) | (__ballot(r[s][1] > t) != 0ull ? 2u : 0u) |
                             (__ballot(r[s][2] > t) != 0ull ? 4u : 0u) | (__ballot(r[s][3] > t) != 0ull ? 8u : 0u);
         if (m4 != 0u) {
-          if (lane == 0) fired[s][nfired[s]] = ((uint32_t)(cbase + (i >> 3)) << 4) | m4;
+          if (lane == 0) fired[s][nfired[s]] = ((uint32_t)(cbase + chunk_of(i)) << 4) | m4;
           ++nfired[s];
         }
         r[s][0] = r[s][1] = r[s][2] = r[s][3] = (int)0x80000000;
@@ -756,7 +802,7 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
 }
 
 template <int C, bool STATS, int W = k16Waves, int G = kGroup, int QS = k16Sets>
-__global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
+__global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
                                                                 const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
                                                                 const int32_t* __restrict__ n_active_p,
@@ -766,6 +812,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
                                                                 int32_t* __restrict__ n_ovf, int plan_rt,
                                                                 int plan_p, int dbg, unsigned long long* gstats) {
   constexpr int NG = W * QS;  // query groups of 32 per workgroup; wave w owns groups w·QS .. w·QS + QS − 1
+  constexpr bool ABL = STATS || FWAV_TOPK_ABL != 0;  // ablation bits honoured
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
   // ALL of the kernel's LDS is one __shared__ object: beside a second one, hipcc waits vmcnt(0) for the in-flight
   // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
@@ -801,7 +848,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
   // 2 = skip MFMA + threshold test, 4 = no global chunk loads, 128 = DMA only every other chunk,
   // 256 = no group barrier, 512 = fold without ballots, 1024 = MFMA without fold, 4096 = record the workgroup
   // timeline (combinable with the others), 8192 = no seeded band limits
-  if (!STATS) dbg = 0;
+  if (!STATS) dbg = FWAV_TOPK_ABL;  // production: 0; ablation builds (-DFWAV_TOPK_ABL=bits) fix the bits at compile time
   half8 b[QS];
   float thf[QS];
   int upd[QS];
@@ -821,7 +868,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
   }
 
   // seed the band limits from the queries' own domain windows (tiles from the wave's first query row)
-  if (!(STATS && (dbg & 8192))) {  // ablation 8192: no seed
+  if (!(ABL && (dbg & 8192))) {  // ablation 8192: no seed
 #pragma unroll
     for (int s = 0; s < QS; ++s) {
       // whole wave (MFMA + shuffles); lanes of unused query slots discard the result
@@ -851,8 +898,8 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     for (int j = 0; j < G; ++j) {
       int64_t c_ = c0 + gg * G + j;
       c_ = c_ < c1 ? c_ : c1 - 1;
-      if (STATS && (dbg & 4)) c_ = 0;  // ablation: no streaming traffic beyond one L2-resident chunk
-      if (STATS && (dbg & 128) && (j & 1)) continue;  // ablation: DMA only every other chunk
+      if (ABL && (dbg & 4)) c_ = 0;  // ablation: no streaming traffic beyond one L2-resident chunk
+      if (ABL && (dbg & 128) && (j & 1)) continue;  // ablation: DMA only every other chunk
       // the chunk's 8 KB = 8 wave-instructions of 64 × 16 B, dealt round-robin over the W waves
       for (int k = wave; k < 8; k += W) {
         // inline asm, not the builtin: hipcc would otherwise wait for this DMA (vmcnt(0)) before every ds_read
@@ -873,7 +920,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
 
   int sink = 0;     // ablation builds: keeps the MFMA / fold results of dbg 512/1024 alive
   int nfired[QS];  // wave-uniform counts of chunks recorded in sm.fired[group] this window
-  int qcnt[QS];    // entries in this lane's query buffer (same value in both lanes of a query)
+  int qcnt[QS];    // this lane's entries in its query's two-ended buffer (h = 0: front, h = 1: back)
 #pragma unroll
   for (int s = 0; s < QS; ++s) nfired[s] = qcnt[s] = 0;
   for (int64_t g = 0; g < ngroups; ++g) {
@@ -884,7 +931,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     // RAW: own DMA of group g retired, then every wave's (barrier).  WAR: the other half was last read in
     // iteration g−1, whose ds_reads were all consumed before its waves reached this barrier.
-    if (!(STATS && (dbg & 256))) {  // ablation 256: no group barrier (LDS races; timing only)
+    if (!(ABL && (dbg & 256))) {  // ablation 256: no group barrier (LDS races; timing only)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -892,19 +939,24 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(7, t_b1 - t_b0);
     if (g + 1 < ngroups) issue_group(g + 1);
-    if (STATS && (dbg & 2)) continue;
+    if (ABL && (dbg & 2)) continue;
     int thi[QS];
 #pragma unroll
     for (int s = 0; s < QS; ++s) thi[s] = int_threshold(thf[s]);
     const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
-    if (STATS && (dbg & (512 | 1024)) && c_end - cg == G) {
+    if (ABL && (dbg & (512 | 1024)) && c_end - cg == G) {
       // ablations 512: fold without ballots, 1024: MFMA without fold (outputs invalid)
       if (dbg & 1024)
         stream_group<G, QS, 2>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane, &sink);
       else
         stream_group<G, QS, 1>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane, &sink);
     } else if (c_end - cg == G) {
-      stream_group<G, QS>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
+#if FWAV_TOPK_STAGGER
+      if (wave >= W / 2)
+        stream_group<G, QS, 0, G / 2>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
+      else
+#endif
+        stream_group<G, QS>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
     } else {
       for (int64_t c = cg; c < c_end; ++c)
         stream_group<1, QS>(lda0 + (c - cg) * 512 * 8, b, thi, c, sm.fired + wave * QS, nfired, lane);
@@ -931,8 +983,12 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
   const unsigned long long t_final = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
   // the final pass reads the counts from LDS (same wave: program order)
 #pragma unroll
-  for (int s = 0; s < QS; ++s)
-    if (h == 0) sm.cnt[(wave * QS + s) * 32 + col] = qcnt[s];
+  for (int s = 0; s < QS; ++s) {
+    if (h == 0)
+      sm.cnt[(wave * QS + s) * 32 + col] = qcnt[s];
+    else
+      sm.cnt1[(wave * QS + s) * 32 + col] = qcnt[s];
+  }
 
   for (int l = 0; l < 32 * QS; ++l) {
     const int qs = wave * QS * 32 + l;
@@ -940,22 +996,18 @@ __global__ __launch_bounds__(64 * W, 4) void k_sim_topk_f16(const _Float16* __re
     if (qq >= n_active) break;
     const int32_t qid = active[qq];
     uint64_t* kq = gkeys + (size_t)qs * C;
-    if (lane == 0) FWAV_TRACE(sm.qrow[qs], 3u, (uint32_t)sm.cnt[qs], (uint32_t)sm.ovf[qs], 0u);
-    compact16<C>(kq, sm, qs, K, emb, STATS ? stats : nullptr);  // exact f32 rescoring of the kept band + sort
-    const int n = sm.cnt[qs];
+    if (lane == 0) FWAV_TRACE(sm.qrow[qs], 3u, (uint32_t)sm.cnt[qs], (uint32_t)sm.ovf[qs], (uint32_t)sm.cnt1[qs]);
+    // exact f32 rescoring of the kept band + sort; a piece keeps its top K in the buffer, the overflow flag in the
+    // last entry (k_merge_pieces combines the block's pieces)
+    compact16<C>(kq, sm, qs, K, emb, npieces == 1 ? cand + (int64_t)qid * K : nullptr);
     if (npieces == 1) {
-      int32_t* out = cand + (int64_t)qid * K;
-      for (int e = lane; e < K; e += 64) out[e] = e < n ? key_idx(kq[e]) : -1;
       if (lane == 0 && sm.ovf[qs]) ovf_list[atomicAdd(n_ovf, 1)] = qid;
-    } else {
-      // a piece: its exact top K stays in the buffer as sorted f32 keys (0-padded), the overflow flag in the
-      // last entry; k_merge_pieces combines the block's pieces
-      for (int e = n + lane; e < K; e += 64) kq[e] = 0ull;
-      if (lane == 0) kq[C - 1] = sm.ovf[qs] ? 1ull : 0ull;
+    } else if (lane == 0) {
+      kq[C - 1] = sm.ovf[qs] ? 1ull : 0ull;
     }
   }
+  if (ABL && sink == 0x7fffffff) cand[0] = sink;
   if (STATS) {
-    if (sink == 0x7fffffff) cand[0] = sink;
     stat_add(8, __builtin_amdgcn_s_memrealtime() - t_final);
     stat_add(6, __builtin_amdgcn_s_memrealtime() - t_kernel);
     if (gstats != nullptr && lane < kStats) atomicAdd(gstats + lane, sm.wstat[wave][lane]);

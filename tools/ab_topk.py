@@ -37,7 +37,12 @@ call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(),
 nq = int(os.environ.get("AB_NQ", nr))  # active queries (default: all ranges)
 active = torch.arange(nq, dtype=torch.int32, device="cuda")
 n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
-wsn = size_call("fwav_sim_topk_workspace_size", nr, nd, 64)
+# each build's plan (and so its workspace) depends on its own occupancy: size for the largest
+wsn = 0
+for _, L in libs:
+    L.fwav_sim_topk_workspace_size.restype = C.c_size_t
+    L.fwav_sim_topk_workspace_size.argtypes = [C.c_int64, C.c_int64, C.c_int]
+    wsn = max(wsn, L.fwav_sim_topk_workspace_size(nr, nd, 64))
 wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
 outs = {}
 times = {n: [] for n, _ in libs}

@@ -68,14 +68,19 @@ dif = np.nonzero(sd0 != sd1)[0]
 print("queries whose two lanes got different seeds:", len(dif), dif[:20], sd0[dif[:5]], sd1[dif[:5]])
 for t, a, b, d in ev:
     if t == 1:
-        dt, h, mask, qcnt = int(a), int(b >> 16), int(b & 0xffff), int(d)
-        doms = [dt + 4 * h + (rr & 3) + 8 * (rr >> 2) for rr in range(16) if mask >> rr & 1]
-        appended.update(doms)
-        print(f"  append dt={dt} h={h} qcnt={qcnt} n={len(doms)} doms={doms[:6]}{'...' if len(doms) > 6 else ''}")
+        dt, h, rr, slot = int(a), int(b >> 16), int(b & 0xffff), int(d)  # one appended row (two-ended buffer)
+        dom = dt + 4 * h + (rr & 3) + 8 * (rr >> 2)
+        appended.add(dom)
+        print(f"  append dom={dom} h={h} slot={slot}")
     elif t == 2:
         print(f"  compact n={a} lim={np.uint32(b).view(np.float32):.6f} m={d & 0xffff} ovf={d >> 16}")
     elif t == 3:
-        print(f"  final cnt={a} ovf={b}")
+        print(f"  final cnt={a} cnt1={d} ovf={b}")
 miss = sorted(set(ref[Q]) - set(c[Q]))
 print("missing domains ever appended:", [m for m in miss if m in appended])
+# the query's key buffer after the kernel (plan (0, 1): item = block Q // 256, 256 entries per query)
+kb = wsk.cpu().numpy()[:(Q // 256 + 1) * 256 * 256 * 8].view(np.uint64).reshape(-1, 256)[Q]
+idx = lambda k: int(np.uint32(~np.uint32(k & np.uint64(0xffffffff))).view(np.int32))  # noqa: E731
+print("buffer front (final top K):", [idx(k) if k else None for k in kb[:K]])
+print("buffer back:", [(255 - i, idx(kb[255 - i]) if kb[255 - i] else None) for i in range(48)])
 L.fwav_debug_topk_plan(-1, 1)
