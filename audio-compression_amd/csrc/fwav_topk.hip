@@ -299,6 +299,14 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_ABL
 #define FWAV_TOPK_ABL 0
 #endif
+// RING: no workgroup barrier in the stream.  The chunk slots form a ring of 8 / G group slots with LDS counters:
+// a wave that finds the next group's slot free (every wave has left the group that occupied it) claims the group
+// and issues its whole DMA, then publishes it as landed once its own vmcnt drains; a wave streams group g as soon
+// as g is landed.  Waves may drift apart by up to (8 / G − 1) groups, so one wave's window replay no longer holds
+// the other seven at the next barrier.
+#ifndef FWAV_TOPK_RING
+#define FWAV_TOPK_RING 0
+#endif
 // STAGGER: the second half of the waves takes each group's chunks in rotated order (A/B at cfg2: 22.85 → 22.46 ms;
 // a static s_setprio for that half instead was slower, 23.50 ms)
 #ifndef FWAV_TOPK_STAGGER
@@ -347,6 +355,10 @@ __host__ __device__ inline void plan_item(const TopkPlan& pl, int64_t item, int6
 #define FWAV_TOPK_WARM 64
 #endif
 constexpr int kWindowGroups = FWAV_TOPK_WIN;  // after the warm-up, fired chunks are replayed every 16 groups (64 chunks)
+// fired-chunk FIFO per query group (a ring; power of two).  Measured and rejected (cfg2 A/B, identical outputs):
+// replaying B ≤ 4 pending tiles per group with prefetched fragments instead of whole windows (27–32 ms vs 22.9:
+// the band limit then rises too late), and windows at doubling stream lengths (28.0 vs 21.7 ms).
+constexpr int kFifo = kWindowGroups * 4;
 constexpr int kWarmChunks = FWAV_TOPK_WARM;   // ... and after every group during the first 64 chunks
 
 
@@ -392,7 +404,7 @@ struct Topk16SmemT {
   int cnt1[32 * NG];  // ... and at the back (its h = 1 lane's)
   int ovf[32 * NG];  // band overflowed the buffer: recompute this query with the f32 kernel
   int64_t qrow[32 * NG];
-  uint32_t fired[NG][kWindowGroups * 4];           // per-group deferred work: chunk indices of a window
+  uint32_t fired[NG][kFifo];                       // deferred work: ring of fired chunk entries
   unsigned long long wstat[STATS ? NG : 1][kStats];  // STATS builds only (one row per wave)
 };
 
@@ -630,42 +642,47 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
 // batch's fragment loads (from the fp16 table, L2/MALL-resident) are issued together, so a window costs
 // ~one memory round trip per batch instead of one per chunk, and tiles of quiet chains are not recomputed.
 constexpr int kReplayBatch = 8;
+// Cursor over a query group's pending fired tiles: FIFO entries [head, tail) of `fired` (a ring), the entry being
+// expanded (chunk cc, tiles rem).  Wave-uniform.
+struct ReplayCursor {
+  int head;
+  int64_t cc;
+  uint32_t rem;
+};
+// Next pending tile (its first domain), or −1.
+__device__ __forceinline__ int64_t next_tile(ReplayCursor& cur, int tail, const uint32_t* fired) {
+  while (cur.rem == 0u && cur.head < tail) {
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane(fired[cur.head++ & (kFifo - 1)]);
+    cur.cc = e >> 4;
+    cur.rem = (e & 15u) | ((e & 15u) << 4);
+  }
+  if (cur.rem == 0u) return -1;
+  const int t = __builtin_ctz(cur.rem);
+  cur.rem &= cur.rem - 1;
+  return cur.cc * kChunk + t * 32;
+}
+__device__ __forceinline__ half8 tile_fragment(const _Float16* __restrict__ emb16, int64_t dt, int h, int col) {
+  const int64_t c = dt / kChunk, t = (dt % kChunk) / 32;
+  return *reinterpret_cast<const half8*>(emb16 + ((c * 2 + h) * kChunk + col) * 8 + t * 256);
+}
+
 template <int C, bool STATS, class SM>
-__device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int& qcnt, int nf,
-                                               int64_t nd, uint64_t* __restrict__ gkeys, SM& sm, int qg, int K,
-                                               int upd, unsigned long long* stats) {
+__device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int& qcnt,
+                                               ReplayCursor& cur, int tail, int64_t nd, uint64_t* __restrict__ gkeys,
+                                               SM& sm, int qg, int K, int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
   const int col = lane & 31;
   const int h = lane >> 5;
-  int i = 0;           // next entry
-  uint32_t rem = 0;    // tiles of the current entry still to replay
-  int64_t cc = 0;      // current entry's chunk
-  if (STATS) stat_add(0, nf);
+  if (STATS) stat_add(0, tail - cur.head);
   while (true) {
     int64_t ct[kReplayBatch];  // tile start domain, −1 = none
 #pragma unroll
-    for (int u = 0; u < kReplayBatch; ++u) {
-      while (rem == 0u && i < nf) {
-        const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane(sm.fired[qg][i++]);
-        cc = e >> 4;
-        rem = (e & 15u) | ((e & 15u) << 4);
-      }
-      if (rem != 0u) {
-        const int t = __builtin_ctz(rem);
-        rem &= rem - 1;
-        ct[u] = cc * kChunk + t * 32;
-      } else {
-        ct[u] = -1;
-      }
-    }
+    for (int u = 0; u < kReplayBatch; ++u) ct[u] = next_tile(cur, tail, sm.fired[qg]);
     if (ct[0] < 0) break;
     half8 af[kReplayBatch];
 #pragma unroll
-    for (int u = 0; u < kReplayBatch; ++u) {
-      const int64_t dt = ct[u] < 0 ? ct[0] : ct[u];  // unconditional loads (no wait on the spot)
-      const int64_t c = dt / kChunk, t = (dt % kChunk) / 32;
-      af[u] = *reinterpret_cast<const half8*>(emb16 + ((c * 2 + h) * kChunk + col) * 8 + t * 256);
-    }
+    for (int u = 0; u < kReplayBatch; ++u)  // unconditional loads (no wait on the spot)
+      af[u] = tile_fragment(emb16, ct[u] < 0 ? ct[0] : ct[u], h, col);
     if (STATS) {  // time the fragment round trip (timing build only: forces the wait here)
       const unsigned long long t_l0 = __builtin_amdgcn_s_memrealtime();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -750,7 +767,7 @@ __device__ __forceinline__ float seed_limit(const _Float16* __restrict__ emb16, 
 // two halves of the workgroup, which otherwise reach their MFMA and fold phases in lockstep.
 template <int NC, int QS, int MODE = 0, int ROT = 0>
 __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, const half8 (&b)[QS],
-                                             const int (&thi)[QS], int64_t cbase, uint32_t (*fired)[kWindowGroups * 4],
+                                             const int (&thi)[QS], int64_t cbase, uint32_t (*fired)[kFifo],
                                              int (&nfired)[QS], int lane, int* sink = nullptr) {
   constexpr int NT = 8 * NC;
   constexpr int kChunkHalfs = 512 * 8;  // one 8 KB chunk slot
@@ -792,7 +809,7 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
         const uint32_t m4 = (__ballot(r[s][0] > t) != 0ull ? 1u : 0u) | (__ballot(r[s][1] > t) != 0ull ? 2u : 0u) |
                             (__ballot(r[s][2] > t) != 0ull ? 4u : 0u) | (__ballot(r[s][3] > t) != 0ull ? 8u : 0u);
         if (m4 != 0u) {
-          if (lane == 0) fired[s][nfired[s]] = ((uint32_t)(cbase + chunk_of(i)) << 4) | m4;
+          if (lane == 0) fired[s][nfired[s] & (kFifo - 1)] = ((uint32_t)(cbase + chunk_of(i)) << 4) | m4;
           ++nfired[s];
         }
         r[s][0] = r[s][1] = r[s][2] = r[s][3] = (int)0x80000000;
@@ -816,9 +833,14 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
   // ALL of the kernel's LDS is one __shared__ object: beside a second one, hipcc waits vmcnt(0) for the in-flight
   // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
+  constexpr bool kRing = FWAV_TOPK_RING != 0;
+  constexpr int NGS = kRing ? 8 / G : 2;  // group slots
   struct Lds {
-    u32x4 slots[2 * G][512];
+    u32x4 slots[NGS * G][512];
     Topk16SmemT<NG, STATS> sm;
+    uint32_t ring_landed[NGS];  // RING: index + 1 of the group whose DMA has landed in the slot
+    uint32_t ring_left[NGS];    // RING: waves that have finished reading the slot (monotonic: W per generation)
+    uint32_t ring_next;         // RING: next group to claim
   };
   __shared__ __attribute__((aligned(16))) Lds lds_all;
   u32x4(*slots)[512] = lds_all.slots;
@@ -916,18 +938,131 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
   // retire the prologue's ordinary loads (query fragments, active list) before the stream, visibly to hipcc
   // (a load still pending at the loop head is waited on, vmcnt(0), inside every chunk iteration)
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  if (ngroups > 0) issue_group(0);
+  if (!kRing && ngroups > 0) issue_group(0);
 
   int sink = 0;     // ablation builds: keeps the MFMA / fold results of dbg 512/1024 alive
-  int nfired[QS];  // wave-uniform counts of chunks recorded in sm.fired[group] this window
+  int nfired[QS];  // wave-uniform FIFO tail: chunks recorded in sm.fired[group] so far
+  ReplayCursor cur[QS];
   int qcnt[QS];    // this lane's entries in its query's two-ended buffer (h = 0: front, h = 1: back)
 #pragma unroll
-  for (int s = 0; s < QS; ++s) nfired[s] = qcnt[s] = 0;
+  for (int s = 0; s < QS; ++s) {
+    nfired[s] = qcnt[s] = 0;
+    cur[s] = ReplayCursor{0, 0, 0u};
+  }
+  if constexpr (kRing) {
+    // ---------------------------------------------------------------- barrier-free ring (FWAV_TOPK_RING)
+    if (tid < NGS) {
+      lds_all.ring_landed[tid] = 0u;
+      lds_all.ring_left[tid] = 0u;
+    }
+    if (tid == 0) lds_all.ring_next = 0u;
+    __syncthreads();  // counters (and the prologue's sm writes) visible to every wave
+    auto ld_acq = [](uint32_t* p) {
+      return (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
+    // a claimed group: all 8·G DMA wave-instructions by the claiming wave
+    auto issue_whole = [&](int64_t gg) {
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        int64_t c_ = c0 + gg * G + j;
+        c_ = c_ < c1 ? c_ : c1 - 1;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const unsigned lds_dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(
+              (__attribute__((address_space(3))) void*)(&slots[(gg % NGS) * G + j][k * 64])));
+          const u32x4* gsrc = src + c_ * 512 + k * 64 + lane;
+          unsigned keep;
+          asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                       : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+        }
+      }
+    };
+    int64_t pend[NGS];  // groups this wave has issued but not yet published (wave-uniform)
+    int npend = 0;
+    auto publish = [&]() {
+      if (npend == 0) return;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
+      for (int i = 0; i < npend; ++i)
+        if (lane == 0)
+          __hip_atomic_store(&lds_all.ring_landed[pend[i] % NGS], (uint32_t)(pend[i] + 1), __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      npend = 0;
+    };
+    // claim every group up to `upto` whose slot is free (all W waves have left its previous occupant)
+    auto try_claim = [&](int64_t upto) {
+      while (npend < NGS) {
+        const int64_t c = ld_acq(&lds_all.ring_next);
+        if (c >= ngroups || c > upto) return;
+        if (ld_acq(&lds_all.ring_left[c % NGS]) < (uint32_t)(W * (c / NGS))) return;
+        // claim by compare-and-swap c → c + 1
+        uint32_t expected = (uint32_t)c;
+        bool won = false;
+        if (lane == 0)
+          won = __hip_atomic_compare_exchange_strong(&lds_all.ring_next, &expected, (uint32_t)(c + 1),
+                                                     __ATOMIC_ACQ_REL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane((int)won) == 0) continue;  // another wave took c: try the next one
+        issue_whole(c);
+        pend[npend++] = c;
+      }
+    };
+    for (int64_t g = 0; g < ngroups; ++g) {
+      u32x4(*half)[512] = slots + (g % NGS) * G;
+      const int64_t cg = c0 + g * G;
+      const int64_t c_end = cg + G < c1 ? cg + G : c1;
+      const bool window_end =
+          (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
+      const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+      try_claim(g + NGS - 1);
+      for (int spins = 0; ld_acq(&lds_all.ring_landed[g % NGS]) != (uint32_t)(g + 1); ++spins) {
+        publish();  // the group may be this wave's own
+        try_claim(g + NGS - 1);
+        __builtin_amdgcn_s_sleep(1);
+        if (spins > (1 << 22)) break;  // never expected: bounded so a logic error cannot hang the GPU
+      }
+      const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+      if (STATS) stat_add(7, t_b1 - t_b0);
+      int thi[QS];
+#pragma unroll
+      for (int s = 0; s < QS; ++s) thi[s] = int_threshold(thf[s]);
+      const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
+      if (c_end - cg == G) {
+#if FWAV_TOPK_STAGGER
+        if (wave >= W / 2)
+          stream_group<G, QS, 0, G / 2>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
+        else
+#endif
+          stream_group<G, QS>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
+      } else {
+        for (int64_t c = cg; c < c_end; ++c)
+          stream_group<1, QS>(lda0 + (c - cg) * 512 * 8, b, thi, c, sm.fired + wave * QS, nfired, lane);
+      }
+      // this wave is done with the slot (its ds_reads were consumed by the MFMAs)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0)
+        __hip_atomic_fetch_add(&lds_all.ring_left[g % NGS], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      publish();
+      const unsigned long long t_c = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+      if (STATS) stat_add(9, t_c - t_b1);
+      if (window_end) {
+#pragma unroll
+        for (int s = 0; s < QS; ++s) {
+          if (nfired[s] > cur[s].head || cur[s].rem != 0u)
+            thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], cur[s], nfired[s], nd, gkeys, sm,
+                                             wave * QS + s, K, upd[s], stats);
+        }
+        if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+      }
+    }
+    publish();
+  } else
   for (int64_t g = 0; g < ngroups; ++g) {
     u32x4(*half)[512] = slots + (g & 1) * G;
     const int64_t cg = c0 + g * G;  // first chunk of group g
     const int64_t c_end = cg + G < c1 ? cg + G : c1;
-    const bool window_end = (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
+    const bool window_end =
+        (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
     const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     // RAW: own DMA of group g retired, then every wave's (barrier).  WAR: the other half was last read in
     // iteration g−1, whose ds_reads were all consumed before its waves reached this barrier.
@@ -967,11 +1102,9 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       // each wave replays its own fired chunks (compacting inline when a buffer fills)
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
-        if (nfired[s] > 0) {
-          thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], nfired[s], nd, gkeys, sm, wave * QS + s, K,
-                                           upd[s], stats);
-          nfired[s] = 0;
-        }
+        if (nfired[s] > cur[s].head || cur[s].rem != 0u)
+          thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], cur[s], nfired[s], nd, gkeys, sm,
+                                           wave * QS + s, K, upd[s], stats);
       }
       if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
       // retire the replay's loads and stores here, visibly to hipcc's wait bookkeeping (vmcnt(0) expcnt(7)
