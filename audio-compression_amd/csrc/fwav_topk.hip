@@ -307,10 +307,11 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_RING
 #define FWAV_TOPK_RING 0
 #endif
-// STAGGER: the second half of the waves takes each group's chunks in rotated order (A/B at cfg2: 22.85 → 22.46 ms;
-// a static s_setprio for that half instead was slower, 23.50 ms)
+// STAGGER: 1 = the second half of the waves takes each group's chunks in rotated order, 2 = every wave of a SIMD
+// pair starts on a different chunk.  Neutral in same-box A/B (21.73 / 21.76 / 22.00 ms for 0 / 1 / 2); a static
+// s_setprio for the second half was slower (+3 %).
 #ifndef FWAV_TOPK_STAGGER
-#define FWAV_TOPK_STAGGER 1
+#define FWAV_TOPK_STAGGER 0
 #endif
 constexpr int kGroup = FWAV_TOPK_G;     // chunks per barrier
 constexpr int k16Waves = FWAV_TOPK_W;   // waves per workgroup
@@ -806,9 +807,10 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
         const int t = thi[s];
-        const uint32_t m4 = (__ballot(r[s][0] > t) != 0ull ? 1u : 0u) | (__ballot(r[s][1] > t) != 0ull ? 2u : 0u) |
-                            (__ballot(r[s][2] > t) != 0ull ? 4u : 0u) | (__ballot(r[s][3] > t) != 0ull ? 8u : 0u);
-        if (m4 != 0u) {
+        // one test of the max of the 4 chains first: most chunks fire none
+        if (__ballot(max(max(r[s][0], r[s][1]), max(r[s][2], r[s][3])) > t) != 0ull) {
+          const uint32_t m4 = (__ballot(r[s][0] > t) != 0ull ? 1u : 0u) | (__ballot(r[s][1] > t) != 0ull ? 2u : 0u) |
+                              (__ballot(r[s][2] > t) != 0ull ? 4u : 0u) | (__ballot(r[s][3] > t) != 0ull ? 8u : 0u);
           if (lane == 0) fired[s][nfired[s] & (kFifo - 1)] = ((uint32_t)(cbase + chunk_of(i)) << 4) | m4;
           ++nfired[s];
         }
@@ -838,9 +840,8 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
   struct Lds {
     u32x4 slots[NGS * G][512];
     Topk16SmemT<NG, STATS> sm;
-    uint32_t ring_landed[NGS];  // RING: index + 1 of the group whose DMA has landed in the slot
+    uint32_t ring_landed[NGS];  // RING: waves whose DMA part has landed in the slot (monotonic: W per generation)
     uint32_t ring_left[NGS];    // RING: waves that have finished reading the slot (monotonic: W per generation)
-    uint32_t ring_next;         // RING: next group to claim
   };
   __shared__ __attribute__((aligned(16))) Lds lds_all;
   u32x4(*slots)[512] = lds_all.slots;
@@ -955,20 +956,18 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       lds_all.ring_landed[tid] = 0u;
       lds_all.ring_left[tid] = 0u;
     }
-    if (tid == 0) lds_all.ring_next = 0u;
     __syncthreads();  // counters (and the prologue's sm writes) visible to every wave
     auto ld_acq = [](uint32_t* p) {
       return (uint32_t)__builtin_amdgcn_readfirstlane(
           (int)__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
     };
-    // a claimed group: all 8·G DMA wave-instructions by the claiming wave
-    auto issue_whole = [&](int64_t gg) {
+    // this wave's share of group gg's DMA (the same 8·G / W wave-instructions as the barrier loop)
+    auto issue_part = [&](int64_t gg) {
 #pragma unroll
       for (int j = 0; j < G; ++j) {
         int64_t c_ = c0 + gg * G + j;
         c_ = c_ < c1 ? c_ : c1 - 1;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = wave; k < 8; k += W) {
           const unsigned lds_dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(
               (__attribute__((address_space(3))) void*)(&slots[(gg % NGS) * G + j][k * 64])));
           const u32x4* gsrc = src + c_ * 512 + k * 64 + lane;
@@ -978,33 +977,20 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
         }
       }
     };
-    int64_t pend[NGS];  // groups this wave has issued but not yet published (wave-uniform)
-    int npend = 0;
+    // Groups [pub, iss) have this wave's part issued but not yet counted as landed.  Every wave issues its part of
+    // group c once the slot is free (all W waves have left group c − NGS) and publishes it (ring_landed += 1) after
+    // its own vmcnt drains; group c is readable when ring_landed of its slot reaches W per generation.
+    int64_t iss = 0, pub = 0;
     auto publish = [&]() {
-      if (npend == 0) return;
+      if (pub == iss) return;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
-      for (int i = 0; i < npend; ++i)
+      for (; pub < iss; ++pub)
         if (lane == 0)
-          __hip_atomic_store(&lds_all.ring_landed[pend[i] % NGS], (uint32_t)(pend[i] + 1), __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      npend = 0;
+          __hip_atomic_fetch_add(&lds_all.ring_landed[pub % NGS], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    // claim every group up to `upto` whose slot is free (all W waves have left its previous occupant)
-    auto try_claim = [&](int64_t upto) {
-      while (npend < NGS) {
-        const int64_t c = ld_acq(&lds_all.ring_next);
-        if (c >= ngroups || c > upto) return;
-        if (ld_acq(&lds_all.ring_left[c % NGS]) < (uint32_t)(W * (c / NGS))) return;
-        // claim by compare-and-swap c → c + 1
-        uint32_t expected = (uint32_t)c;
-        bool won = false;
-        if (lane == 0)
-          won = __hip_atomic_compare_exchange_strong(&lds_all.ring_next, &expected, (uint32_t)(c + 1),
-                                                     __ATOMIC_ACQ_REL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (__builtin_amdgcn_readfirstlane((int)won) == 0) continue;  // another wave took c: try the next one
-        issue_whole(c);
-        pend[npend++] = c;
-      }
+    auto try_issue = [&](int64_t upto) {
+      upto = upto < ngroups - 1 ? upto : ngroups - 1;
+      while (iss <= upto && ld_acq(&lds_all.ring_left[iss % NGS]) >= (uint32_t)(W * (iss / NGS))) issue_part(iss++);
     };
     for (int64_t g = 0; g < ngroups; ++g) {
       u32x4(*half)[512] = slots + (g % NGS) * G;
@@ -1013,10 +999,10 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       const bool window_end =
           (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
       const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-      try_claim(g + NGS - 1);
-      for (int spins = 0; ld_acq(&lds_all.ring_landed[g % NGS]) != (uint32_t)(g + 1); ++spins) {
-        publish();  // the group may be this wave's own
-        try_claim(g + NGS - 1);
+      try_issue(g + NGS - 1);
+      for (int spins = 0; ld_acq(&lds_all.ring_landed[g % NGS]) < (uint32_t)(W * (g / NGS + 1)); ++spins) {
+        publish();  // part of the group may be this wave's own
+        try_issue(g + NGS - 1);
         __builtin_amdgcn_s_sleep(1);
         if (spins > (1 << 22)) break;  // never expected: bounded so a logic error cannot hang the GPU
       }
@@ -1068,7 +1054,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
     // iteration g−1, whose ds_reads were all consumed before its waves reached this barrier.
     if (!(ABL && (dbg & 256))) {  // ablation 256: no group barrier (LDS races; timing only)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if (!(ABL && (dbg & 16384))) __builtin_amdgcn_s_barrier();  // 16384: own DMA wait, no barrier
       asm volatile("" ::: "memory");
     }
     const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1086,12 +1072,22 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       else
         stream_group<G, QS, 1>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane, &sink);
     } else if (c_end - cg == G) {
+#if FWAV_TOPK_STAGGER == 2
+      // every wave of a SIMD pair starts the group on a different chunk
+      switch (wave & (G - 1)) {
+        case 0: stream_group<G, QS, 0, 0>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane); break;
+        case 1: stream_group<G, QS, 0, (1 % G)>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane); break;
+        case 2: stream_group<G, QS, 0, (2 % G)>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane); break;
+        default: stream_group<G, QS, 0, (3 % G)>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane); break;
+      }
+#else
 #if FWAV_TOPK_STAGGER
       if (wave >= W / 2)
         stream_group<G, QS, 0, G / 2>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
       else
 #endif
         stream_group<G, QS>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
+#endif
     } else {
       for (int64_t c = cg; c < c_end; ++c)
         stream_group<1, QS>(lda0 + (c - cg) * 512 * 8, b, thi, c, sm.fired + wave * QS, nfired, lane);
