@@ -316,7 +316,12 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 constexpr int kGroup = FWAV_TOPK_G;     // chunks per barrier
 constexpr int k16Waves = FWAV_TOPK_W;   // waves per workgroup
 constexpr int k16Sets = FWAV_TOPK_QS;   // query sets of 32 per wave (each LDS fragment feeds k16Sets MFMAs)
-constexpr int k16Cap = 256;          // key-buffer entries per query (global workspace)
+#ifndef FWAV_TOPK_CAP
+#define FWAV_TOPK_CAP 256
+#endif
+constexpr int k16Cap = FWAV_TOPK_CAP;  // key-buffer entries per query (global workspace)
+static_assert(k16Cap >= 128 && (k16Cap & (k16Cap - 1)) == 0, "the final bitonic sort needs a power-of-two buffer");
+// (A/B at cfg2: 512 entries 24.4 ms vs 21.2 ms for 256 — fewer compactions do not pay for the longer final sort)
 constexpr int k16QB = 32 * k16Waves * k16Sets;  // queries per block (one workgroup's query set)
 constexpr int kMaxPieces = 8;        // a split block's table pieces (merge: P·K ≤ 512 keys per query)
 
