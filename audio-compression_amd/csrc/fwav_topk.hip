@@ -320,6 +320,14 @@ constexpr int k16Sets = FWAV_TOPK_QS;   // query sets of 32 per wave (each LDS f
 #define FWAV_TOPK_CAP 256
 #endif
 constexpr int k16Cap = FWAV_TOPK_CAP;  // key-buffer entries per query (global workspace)
+#ifndef FWAV_TOPK_TRIG
+#define FWAV_TOPK_TRIG (FWAV_TOPK_CAP - 32)
+#endif
+#ifndef FWAV_TOPK_GROW
+#define FWAV_TOPK_GROW 64
+#endif
+constexpr int kTrig = FWAV_TOPK_TRIG;  // early compaction: buffer size ...
+constexpr int kGrow = FWAV_TOPK_GROW;  // ... and growth since the last compaction
 static_assert(k16Cap >= 128 && (k16Cap & (k16Cap - 1)) == 0, "the final bitonic sort needs a power-of-two buffer");
 // (A/B at cfg2: 512 entries 24.4 ms vs 21.2 ms for 256 — fewer compactions do not pay for the longer final sort)
 constexpr int k16QB = 32 * k16Waves * k16Sets;  // queries per block (one workgroup's query set)
@@ -332,26 +340,38 @@ constexpr int kMaxPieces = 8;        // a split block's table pieces (merge: P·
 // its exact top K (f32 keys, sorted), and k_merge_pieces merges a split block's P lists.  Each item owns one
 // key-buffer region (QB queries × C entries).  Every workgroup recomputes the plan from the device-side active
 // count, so the launch needs no host sync; the grid and workspace cover the plan of max_q.
+// P < 0 selects query halves instead of table pieces: each of the last R blocks becomes two items of half its
+// queries (W/2 waves, the other waves exit at once) that stream the whole table — no merge, no restarted limits, and a
+// half block on a CU of its own runs its waves faster than a full block.
 struct TopkPlan {
   int64_t nb, F, R;
   int P;
+  bool halves;
   __host__ __device__ int64_t items() const { return F + R * P; }
 };
 __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P) {
   TopkPlan pl;
   pl.nb = cdiv(n_queries > 0 ? n_queries : 0, k16QB);
-  pl.P = P < 1 ? 1 : (P > kMaxPieces ? kMaxPieces : P);
+  pl.halves = P < 0;
+  pl.P = pl.halves ? 2 : (P < 1 ? 1 : (P > kMaxPieces ? kMaxPieces : P));
   pl.R = pl.P == 1 ? 0 : (pl.nb < rt ? pl.nb : (int64_t)rt);
   pl.F = pl.nb - pl.R;
   return pl;
 }
-// item → (block, piece, pieces)
-__host__ __device__ inline void plan_item(const TopkPlan& pl, int64_t item, int64_t& block, int& piece, int& np) {
+// item → (block, table piece, table pieces, query half: −1 = the whole block)
+__host__ __device__ inline void plan_item(const TopkPlan& pl, int64_t item, int64_t& block, int& piece, int& np,
+                                          int& qhalf) {
+  qhalf = -1;
   if (item < pl.F) {
     block = item; piece = 0; np = 1;
   } else {
     const int64_t j = item - pl.F;
-    block = pl.F + j / pl.P; piece = (int)(j % pl.P); np = pl.P;
+    block = pl.F + j / pl.P;
+    if (pl.halves) {
+      piece = 0; np = 1; qhalf = (int)(j % 2);
+    } else {
+      piece = (int)(j % pl.P); np = pl.P;
+    }
   }
 }
 #ifndef FWAV_TOPK_WIN
@@ -581,7 +601,7 @@ __device__ __forceinline__ int fold16(int r, const floatx16& a) {
 // survivors (s16 keys) to the wave-owned global key buffers — one LDS atomic per lane reserves the slots,
 // the stores are fire-and-forget — and compact a buffer inline only when it is about to overflow.
 template <int C, bool STATS, class SM>
-__device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int& qcnt, int64_t dt, int64_t nd,
+__device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int& qcnt, int& kept, int64_t dt, int64_t nd,
                                              uint64_t* __restrict__ gkeys, SM& sm, int qg, int K, int upd,
                                              unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
@@ -626,8 +646,9 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
     stat_add(2, __ockl_wfred_add_u32((uint32_t)(qcnt - before)));
     stat_add(10, __builtin_amdgcn_s_memrealtime() - t_a0);
   }
-  // compact when fewer than 32 free slots remain (a tile adds ≤ 16 per lane, ≤ 32 per query)
-  uint64_t need = __ballot(lane < 32 && total > C - 32);
+  // compact when fewer than 32 free slots remain (a tile adds ≤ 16 per lane, ≤ 32 per query) — or, to raise the band
+  // limit sooner, once the buffer passes kTrig and has grown by kGrow since its last compaction
+  uint64_t need = __ballot(lane < 32 && (total > C - 32 || (total > kTrig && total >= kept + kGrow)));
   while (need != 0ull) {
     const int l = __builtin_ctzll(need);
     need &= need - 1;
@@ -637,6 +658,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
                      __builtin_amdgcn_readlane(qcnt, l + 32), sm, qg * 32 + l, K, STATS ? stats : nullptr, m, lim);
     if (col == l) {
       qcnt = h ? 0 : m;  // the kept band is written densely at the front
+      kept = m;
       if (upd) thf = fmaxf(thf, lim);  // the seed may be above a buffer's own limit
     }
   }
@@ -647,7 +669,10 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
 // and j + 4.  The recorded tiles are walked with a wave-uniform cursor in batches of kReplayBatch: all of a
 // batch's fragment loads (from the fp16 table, L2/MALL-resident) are issued together, so a window costs
 // ~one memory round trip per batch instead of one per chunk, and tiles of quiet chains are not recomputed.
-constexpr int kReplayBatch = 8;
+#ifndef FWAV_TOPK_RB
+#define FWAV_TOPK_RB 8
+#endif
+constexpr int kReplayBatch = FWAV_TOPK_RB;
 // Cursor over a query group's pending fired tiles: FIFO entries [head, tail) of `fired` (a ring), the entry being
 // expanded (chunk cc, tiles rem).  Wave-uniform.
 struct ReplayCursor {
@@ -674,7 +699,7 @@ __device__ __forceinline__ half8 tile_fragment(const _Float16* __restrict__ emb1
 
 template <int C, bool STATS, class SM>
 __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int& qcnt,
-                                               ReplayCursor& cur, int tail, int64_t nd, uint64_t* __restrict__ gkeys,
+                                               int& kept, ReplayCursor& cur, int tail, int64_t nd, uint64_t* __restrict__ gkeys,
                                                SM& sm, int qg, int K, int upd, unsigned long long* stats) {
   const int lane = threadIdx.x & 63;
   const int col = lane & 31;
@@ -698,7 +723,7 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
     for (int u = 0; u < kReplayBatch; ++u) {
       if (ct[u] < 0) break;
       const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], b, floatx16{}, 0, 0, 0);
-      thf = append_tile<C, STATS>(acc, thf, qcnt, ct[u], nd, gkeys, sm, qg, K, upd, stats);
+      thf = append_tile<C, STATS>(acc, thf, qcnt, kept, ct[u], nd, gkeys, sm, qg, K, upd, stats);
     }
     if (ct[kReplayBatch - 1] < 0) break;
   }
@@ -855,10 +880,12 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
   const int n_active = *n_active_p;
   const TopkPlan plan = make_plan(n_active, plan_rt, plan_p);
   int64_t block;
-  int piece, npieces;
-  plan_item(plan, blockIdx.x, block, piece, npieces);
+  int piece, npieces, qhalf;
+  plan_item(plan, blockIdx.x, block, piece, npieces, qhalf);
   if (block >= plan.nb) return;
-  const int qbase = (int)(block * 32 * NG);
+  const int Wact = qhalf < 0 ? W : W / 2;  // waves with queries
+  if ((int)(threadIdx.x >> 6) >= Wact) return;
+  const int qbase = (int)(block * 32 * NG) + (qhalf > 0 ? (W / 2) * QS * 32 : 0);
   uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * 32 * NG * C;  // this item's key-buffer region
   const unsigned long long t_kernel = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
 
@@ -904,6 +931,11 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
           (int64_t)((__builtin_amdgcn_readfirstlane((int)sm.qrow[(wave * QS + s) * 32]) - kSeedHalf) >> 5) << 5;
       const float seed = seed_limit(emb16, nd, b[s], sm.qrow[(wave * QS + s) * 32 + col], wbase, K);
       if (upd[s]) thf[s] = seed;
+#ifdef FWAV_TOPK_EXTSEED
+      // experiment builds: a host-computed lower bound per active query (gstats reinterpreted as float[n_active])
+      if (upd[s] && gstats != nullptr && qbase + (wave * QS + s) * 32 + col < n_active)
+        thf[s] = fmaxf(thf[s], reinterpret_cast<const float*>(gstats)[qbase + (wave * QS + s) * 32 + col]);
+#endif
 #ifdef FWAV_TOPK_DEBUG
       if (upd[s] && sm.qrow[(wave * QS + s) * 32 + col] < (1 << 19))
         g_fwav_dbg[sm.qrow[(wave * QS + s) * 32 + col] + (h << 19)] = __float_as_uint(seed);
@@ -928,8 +960,8 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       c_ = c_ < c1 ? c_ : c1 - 1;
       if (ABL && (dbg & 4)) c_ = 0;  // ablation: no streaming traffic beyond one L2-resident chunk
       if (ABL && (dbg & 128) && (j & 1)) continue;  // ablation: DMA only every other chunk
-      // the chunk's 8 KB = 8 wave-instructions of 64 × 16 B, dealt round-robin over the W waves
-      for (int k = wave; k < 8; k += W) {
+      // the chunk's 8 KB = 8 wave-instructions of 64 × 16 B, dealt round-robin over the active waves
+      for (int k = wave; k < 8; k += Wact) {
         // inline asm, not the builtin: hipcc would otherwise wait for this DMA (vmcnt(0)) before every ds_read
         // of the other half; completion is counted by hand at the group top
         const unsigned lds_dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(
@@ -950,9 +982,10 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
   int nfired[QS];  // wave-uniform FIFO tail: chunks recorded in sm.fired[group] so far
   ReplayCursor cur[QS];
   int qcnt[QS];    // this lane's entries in its query's two-ended buffer (h = 0: front, h = 1: back)
+  int kept[QS];    // the query's buffer size after its last compaction
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
-    nfired[s] = qcnt[s] = 0;
+    nfired[s] = qcnt[s] = kept[s] = 0;
     cur[s] = ReplayCursor{0, 0, 0u};
   }
   if constexpr (kRing) {
@@ -972,7 +1005,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       for (int j = 0; j < G; ++j) {
         int64_t c_ = c0 + gg * G + j;
         c_ = c_ < c1 ? c_ : c1 - 1;
-        for (int k = wave; k < 8; k += W) {
+        for (int k = wave; k < 8; k += Wact) {
           const unsigned lds_dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(
               (__attribute__((address_space(3))) void*)(&slots[(gg % NGS) * G + j][k * 64])));
           const u32x4* gsrc = src + c_ * 512 + k * 64 + lane;
@@ -995,7 +1028,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
     };
     auto try_issue = [&](int64_t upto) {
       upto = upto < ngroups - 1 ? upto : ngroups - 1;
-      while (iss <= upto && ld_acq(&lds_all.ring_left[iss % NGS]) >= (uint32_t)(W * (iss / NGS))) issue_part(iss++);
+      while (iss <= upto && ld_acq(&lds_all.ring_left[iss % NGS]) >= (uint32_t)(Wact * (iss / NGS))) issue_part(iss++);
     };
     for (int64_t g = 0; g < ngroups; ++g) {
       u32x4(*half)[512] = slots + (g % NGS) * G;
@@ -1005,7 +1038,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
           (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
       const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
       try_issue(g + NGS - 1);
-      for (int spins = 0; ld_acq(&lds_all.ring_landed[g % NGS]) < (uint32_t)(W * (g / NGS + 1)); ++spins) {
+      for (int spins = 0; ld_acq(&lds_all.ring_landed[g % NGS]) < (uint32_t)(Wact * (g / NGS + 1)); ++spins) {
         publish();  // part of the group may be this wave's own
         try_issue(g + NGS - 1);
         __builtin_amdgcn_s_sleep(1);
@@ -1039,7 +1072,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
 #pragma unroll
         for (int s = 0; s < QS; ++s) {
           if (nfired[s] > cur[s].head || cur[s].rem != 0u)
-            thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], cur[s], nfired[s], nd, gkeys, sm,
+            thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], kept[s], cur[s], nfired[s], nd, gkeys, sm,
                                              wave * QS + s, K, upd[s], stats);
         }
         if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
@@ -1104,7 +1137,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
         if (nfired[s] > cur[s].head || cur[s].rem != 0u)
-          thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], cur[s], nfired[s], nd, gkeys, sm,
+          thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], kept[s], cur[s], nfired[s], nd, gkeys, sm,
                                            wave * QS + s, K, upd[s], stats);
       }
       if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
@@ -1166,7 +1199,7 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   const int n_active = *n_active_p;
   const TopkPlan plan = make_plan(n_active, plan_rt, plan_p);
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // split-block query index
-  if (plan.R == 0 || w >= plan.R * k16QB) return;
+  if (plan.R == 0 || plan.halves || w >= plan.R * k16QB) return;
   const int lane = threadIdx.x & 63;
   const int64_t block = plan.F + w / k16QB;
   const int ql = (int)(w % k16QB);
@@ -1225,7 +1258,7 @@ static void topk_device_slots(int& cus, int& per_cu) {
 // since every piece restarts the rising limit: 268 blocks in 2 pieces 24.2 ms, 512 in 2 25.3 ms).  Few blocks
 // (at most half the slots) are each split into up to 8 pieces so that the table passes use the idle CUs.
 static void host_plan_for(int64_t max_q, int64_t nd, int& rt, int& P) {
-  if (g_plan_rt >= 0 && g_plan_p >= 1) {
+  if (g_plan_rt >= 0) {  // diagnostic override
     rt = g_plan_rt;
     P = g_plan_p;
   } else {
@@ -1282,6 +1315,12 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     int rt, P;
     host_plan_for(max_q, nd, rt, P);
     const TopkPlan pl = make_plan(max_q, rt, P);
+#ifdef FWAV_TOPK_EXTSEED
+    if (stats != nullptr && dbg == 0)
+      k_sim_topk_f16<k16Cap, false><<<pl.items(), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, 0, stats);
+    else
+#endif
     if (stats != nullptr || (dbg & 65535) != 0)
       k_sim_topk_f16<k16Cap, true><<<pl.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, dbg & 65535, stats);
@@ -1378,7 +1417,8 @@ int fwav_debug_dump(void* host, size_t bytes, unsigned* n_events) {
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.
 int fwav_debug_topk_plan(int rt, int pieces) {
-  FWAV_CHECK_ARG(pieces >= 1 && pieces <= kMaxPieces, FWAV_ERR_ARG, "fwav_debug_topk_plan: pieces outside [1, 8]");
+  FWAV_CHECK_ARG(pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces), FWAV_ERR_ARG,
+                 "fwav_debug_topk_plan: pieces outside [1, 8] (or -1: query halves)");
   g_plan_rt = rt;
   g_plan_p = rt < 0 ? -1 : pieces;
   return FWAV_OK;

@@ -204,10 +204,11 @@ def test_large_k_vs_oracle(K):
     assert not bad.any(), f"K={K}: {bad.sum()} unexplained mismatches"
 
 
-@pytest.mark.parametrize("plan", [(0, 1), (1 << 20, 2), (1 << 20, 5), (1 << 20, 8), (10, 3)])
+@pytest.mark.parametrize("plan", [(0, 1), (1 << 20, 2), (1 << 20, 5), (1 << 20, 8), (10, 3), (1 << 20, -1), (7, -1)])
 def test_f16_split_plans_equal_f32(plan):
-    """Work plans that split query blocks into table pieces (merged by k_merge_pieces) return exactly the
-    unsplit search's candidates: whole, all blocks in 2/5/8 pieces, and only the last 10 blocks in 3."""
+    """Work plans that split query blocks into table pieces (merged by k_merge_pieces) or into query halves return
+    exactly the unsplit search's candidates: whole, all blocks in 2/5/8 pieces, only the last 10 blocks in 3, and all /
+    the last 7 blocks as two half-blocks (4 waves each; the other waves exit at once)."""
     from fwav import synth
     sig = synth.noise(6.0, 44100, seed=11)
     b, _ = _cands(sig, 2048, 64, "f32")

@@ -1,0 +1,64 @@
+"""Experiment (tools only): how much would a tighter initial band limit help?  Seeds every query with the K-th best
+exact score over a sample of S domains (minus 3δ, a valid s16 lower bound) computed on the host side with torch, and
+times an -DFWAV_TOPK_EXTSEED build with and without them.  usage: python tools/seed_ab.py tools/ab/libfwav_ext.so S..."""
+import ctypes as C
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd")]
+import numpy as np
+import torch
+
+import __graft_entry__
+
+__graft_entry__.build()
+from fwav import engine, synth  # noqa: E402
+from fwav._lib import SIGNATURES, call  # noqa: E402
+
+L = C.CDLL(os.path.abspath(sys.argv[1]))
+for n in ("fwav_debug_sim_topk", "fwav_sim_topk_workspace_size"):
+    getattr(L, n).restype, getattr(L, n).argtypes = SIGNATURES[n]
+sig = torch.from_numpy(synth.noise(60.0, 44100)).cuda()
+r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
+torch.cuda.synchronize()
+nd, nr = r.n_domains, r.n_ranges
+emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+tab = engine.embed_tables(8, torch.device("cuda"))
+pool = torch.empty(nd * 8, device="cuda")
+emb = torch.empty(nd * 16, device="cuda")
+ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
+     emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+active = torch.arange(nr, dtype=torch.int32, device="cuda")
+n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
+wsn = L.fwav_sim_topk_workspace_size(nr, nd, 64)
+wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
+E = emb.view(nd, 16)
+ref = None
+for S in [0] + [int(x) for x in sys.argv[2:]]:
+    seeds = torch.full((nr,), -float("inf"), device="cuda")
+    if S > 0:
+        samp = torch.linspace(0, nd - 1, S, device="cuda").long()
+        Es = E[samp].double()
+        for a in range(0, nr, 32768):
+            sc = E[a:min(a + 32768, nr)].double() @ Es.T
+            seeds[a:a + 32768] = (sc.topk(64, dim=1).values[:, -1] - 3 * 2.5e-3).float()
+    times = []
+    for rep in range(4):
+        cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = L.fwav_debug_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
+                                   64, cand.data_ptr(), wsk.data_ptr(), 0, seeds.data_ptr(), st)
+        e1.record()
+        torch.cuda.synchronize()
+        assert rc == 0
+        if rep:
+            times.append(e0.elapsed_time(e1))
+    if ref is None:
+        ref = cand.clone()
+    print(f"sample {S:6d}: median {np.median(times):7.2f} ms  seed mean {seeds[seeds > -1e30].mean().item() if S else float('nan'):.4f}"
+          f"  identical={bool(torch.equal(cand, ref))}", flush=True)
