@@ -358,6 +358,19 @@ __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P) 
   pl.F = pl.nb - pl.R;
   return pl;
 }
+// Query (position in the active list) of slot ql = group·32 + col of query block `block`.  INTERLEAVE: a block's
+// query groups come from different regions of the list (group g of block b is query group g·nb + b), so every block
+// mixes regions and block run times even out, which shortens the launch's tail.
+#ifndef FWAV_TOPK_INTERLEAVE
+#define FWAV_TOPK_INTERLEAVE 1
+#endif
+__host__ __device__ inline int64_t slot_query(int64_t block, int ql, int64_t nb) {
+#if FWAV_TOPK_INTERLEAVE
+  return ((int64_t)(ql >> 5) * nb + block) * 32 + (ql & 31);
+#else
+  return block * k16QB + ql;
+#endif
+}
 // item → (block, table piece, table pieces, query half: −1 = the whole block)
 __host__ __device__ inline void plan_item(const TopkPlan& pl, int64_t item, int64_t& block, int& piece, int& np,
                                           int& qhalf) {
@@ -885,7 +898,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
   if (block >= plan.nb) return;
   const int Wact = qhalf < 0 ? W : W / 2;  // waves with queries
   if ((int)(threadIdx.x >> 6) >= Wact) return;
-  const int qbase = (int)(block * 32 * NG) + (qhalf > 0 ? (W / 2) * QS * 32 : 0);
+  const int qslot0 = qhalf > 0 ? (W / 2) * QS * 32 : 0;  // the second half block's first query slot
   uint64_t* gkeys = gkeys_all + (size_t)blockIdx.x * 32 * NG * C;  // this item's key-buffer region
   const unsigned long long t_kernel = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
 
@@ -910,7 +923,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     const int ql = (wave * QS + s) * 32 + col;
-    const int qi = qbase + ql;
+    const int64_t qi = slot_query(block, qslot0 + ql, plan.nb);
     const int32_t q = qi < n_active ? active[qi] : -1;
     const int64_t qrow = (int64_t)(q < 0 ? 0 : q) + q_offset;
     b[s] = *reinterpret_cast<const half8*>(emb16 + (((qrow >> 8) * 2 + h) * 256 + (qrow & 255)) * 8);
@@ -933,15 +946,15 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       if (upd[s]) thf[s] = seed;
 #ifdef FWAV_TOPK_EXTSEED
       // experiment builds: a host-computed lower bound per active query (gstats reinterpreted as float[n_active])
-      if (upd[s] && gstats != nullptr && qbase + (wave * QS + s) * 32 + col < n_active)
-        thf[s] = fmaxf(thf[s], reinterpret_cast<const float*>(gstats)[qbase + (wave * QS + s) * 32 + col]);
+      if (upd[s] && gstats != nullptr)
+        thf[s] = fmaxf(thf[s], reinterpret_cast<const float*>(gstats)[slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb)]);
 #endif
 #ifdef FWAV_TOPK_DEBUG
       if (upd[s] && sm.qrow[(wave * QS + s) * 32 + col] < (1 << 19))
         g_fwav_dbg[sm.qrow[(wave * QS + s) * 32 + col] + (h << 19)] = __float_as_uint(seed);
 #endif
       if (STATS && (dbg & 32768) && gstats != nullptr && h == 0 && upd[s])  // diagnostics: the seeds
-        gstats[16 + qbase + (wave * QS + s) * 32 + col] = __float_as_uint(seed);
+        gstats[16 + slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb)] = __float_as_uint(seed);
     }
   }
   const int64_t nchunks = cdiv(nd, kChunk);
@@ -1159,8 +1172,8 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
 
   for (int l = 0; l < 32 * QS; ++l) {
     const int qs = wave * QS * 32 + l;
-    const int qq = qbase + qs;
-    if (qq >= n_active) break;
+    const int64_t qq = slot_query(block, qslot0 + qs, plan.nb);
+    if (qq >= n_active) continue;
     const int32_t qid = active[qq];
     uint64_t* kq = gkeys + (size_t)qs * C;
     if (lane == 0) FWAV_TRACE(sm.qrow[qs], 3u, (uint32_t)sm.cnt[qs], (uint32_t)sm.ovf[qs], (uint32_t)sm.cnt1[qs]);
@@ -1203,7 +1216,7 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   const int lane = threadIdx.x & 63;
   const int64_t block = plan.F + w / k16QB;
   const int ql = (int)(w % k16QB);
-  const int64_t qq = block * k16QB + ql;
+  const int64_t qq = slot_query(block, ql, plan.nb);
   if (qq >= n_active) return;
   const int P = plan.P;
   uint64_t v[E];
