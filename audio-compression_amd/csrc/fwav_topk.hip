@@ -678,7 +678,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
   return thf;
 }
 
-// Window end: replay what this wave recorded.  An entry is (chunk << 4 | chain mask); chain j covers tiles j
+// Window end: replay what this wave recorded.  An entry is (chunk << 8 | chain mask); with 4 chains chain j covers tiles j
 // and j + 4.  The recorded tiles are walked with a wave-uniform cursor in batches of kReplayBatch: all of a
 // batch's fragment loads (from the fp16 table, L2/MALL-resident) are issued together, so a window costs
 // ~one memory round trip per batch instead of one per chunk, and tiles of quiet chains are not recomputed.
@@ -693,12 +693,19 @@ struct ReplayCursor {
   int64_t cc;
   uint32_t rem;
 };
+// Fold chains per 256-domain chunk: tile t folds into chain t % kChains; a fired chunk is recorded as
+// (chunk << 8 | chain mask) and its replay recomputes the tiles of the firing chains (8 / kChains tiles per chain).
+#ifndef FWAV_TOPK_CHAINS
+#define FWAV_TOPK_CHAINS 8
+#endif
+constexpr int kChains = FWAV_TOPK_CHAINS;
+static_assert(kChains == 4 || kChains == 8, "4 or 8 chains per chunk");
 // Next pending tile (its first domain), or −1.
 __device__ __forceinline__ int64_t next_tile(ReplayCursor& cur, int tail, const uint32_t* fired) {
   while (cur.rem == 0u && cur.head < tail) {
     const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane(fired[cur.head++ & (kFifo - 1)]);
-    cur.cc = e >> 4;
-    cur.rem = (e & 15u) | ((e & 15u) << 4);
+    cur.cc = e >> 8;
+    cur.rem = kChains == 8 ? (e & 255u) : ((e & 15u) | ((e & 15u) << 4));
   }
   if (cur.rem == 0u) return -1;
   const int t = __builtin_ctz(cur.rem);
@@ -825,24 +832,29 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
   for (int i = 0; i < 3 && i < NT; ++i) a[i] = rd(i);
 #pragma unroll
   for (int s = 0; s < QS; ++s) acc[0][s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[s], floatx16{}, 0, 0, 0);
-  int r[QS][4];
+  int r[QS][kChains];
 #pragma unroll
-  for (int s = 0; s < QS; ++s) r[s][0] = r[s][1] = r[s][2] = r[s][3] = (int)0x80000000;
+  for (int s = 0; s < QS; ++s)
+#pragma unroll
+    for (int c = 0; c < kChains; ++c) r[s][c] = (int)0x80000000;
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     if (i + 3 < NT) a[i + 3] = rd(i + 3);
 #pragma unroll
     for (int s = 0; s < QS; ++s) {
       if (i + 1 < NT) acc[i + 1][s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i + 1], b[s], floatx16{}, 0, 0, 0);
+      constexpr int cm = kChains - 1;
       if (MODE & 2)
-        r[s][i & 3] = max(max(r[s][i & 3], __float_as_int(acc[i][s][0])), __float_as_int(acc[i][s][15]));
+        r[s][i & cm] = max(max(r[s][i & cm], __float_as_int(acc[i][s][0])), __float_as_int(acc[i][s][15]));
       else
-        r[s][i & 3] = fold16(r[s][i & 3], acc[i][s]);
+        r[s][i & cm] = fold16(r[s][i & cm], acc[i][s]);
     }
     if (MODE != 0) {
       if (i == NT - 1) {
 #pragma unroll
-        for (int s = 0; s < QS; ++s) *sink ^= r[s][0] ^ r[s][1] ^ r[s][2] ^ r[s][3];
+        for (int s = 0; s < QS; ++s)
+#pragma unroll
+          for (int c = 0; c < kChains; ++c) *sink ^= r[s][c];
       }
       continue;
     }
@@ -850,14 +862,19 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
         const int t = thi[s];
-        // one test of the max of the 4 chains first: most chunks fire none
-        if (__ballot(max(max(r[s][0], r[s][1]), max(r[s][2], r[s][3])) > t) != 0ull) {
-          const uint32_t m4 = (__ballot(r[s][0] > t) != 0ull ? 1u : 0u) | (__ballot(r[s][1] > t) != 0ull ? 2u : 0u) |
-                              (__ballot(r[s][2] > t) != 0ull ? 4u : 0u) | (__ballot(r[s][3] > t) != 0ull ? 8u : 0u);
-          if (lane == 0) fired[s][nfired[s] & (kFifo - 1)] = ((uint32_t)(cbase + chunk_of(i)) << 4) | m4;
+        // one test of the max of the chains first: most chunks fire none
+        int rm = r[s][0];
+#pragma unroll
+        for (int c = 1; c < kChains; ++c) rm = max(rm, r[s][c]);
+        if (__ballot(rm > t) != 0ull) {
+          uint32_t mk = 0u;
+#pragma unroll
+          for (int c = 0; c < kChains; ++c) mk |= __ballot(r[s][c] > t) != 0ull ? (1u << c) : 0u;
+          if (lane == 0) fired[s][nfired[s] & (kFifo - 1)] = ((uint32_t)(cbase + chunk_of(i)) << 8) | mk;
           ++nfired[s];
         }
-        r[s][0] = r[s][1] = r[s][2] = r[s][3] = (int)0x80000000;
+#pragma unroll
+        for (int c = 0; c < kChains; ++c) r[s][c] = (int)0x80000000;
       }
     }
   }
