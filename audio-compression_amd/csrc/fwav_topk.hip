@@ -387,18 +387,21 @@ __host__ __device__ inline void plan_item(const TopkPlan& pl, int64_t item, int6
     }
   }
 }
+// Window schedule (A/B at cfg2 with 8 chains: 16 groups / 64 warm chunks 21.17 ms, 32 / 64 20.92, 16 / 32 20.85,
+// 32 / 32 20.67, 32 / 16 20.70; 8 groups 20.68 vs 20.26 on a faster box)
 #ifndef FWAV_TOPK_WIN
-#define FWAV_TOPK_WIN 16
+#define FWAV_TOPK_WIN 32
 #endif
 #ifndef FWAV_TOPK_WARM
-#define FWAV_TOPK_WARM 64
+#define FWAV_TOPK_WARM 32
 #endif
-constexpr int kWindowGroups = FWAV_TOPK_WIN;  // after the warm-up, fired chunks are replayed every 16 groups (64 chunks)
+constexpr int kWindowGroups = FWAV_TOPK_WIN;  // after the warm-up, fired chunks are replayed every 32 groups (128 chunks)
 // fired-chunk FIFO per query group (a ring; power of two).  Measured and rejected (cfg2 A/B, identical outputs):
 // replaying B ≤ 4 pending tiles per group with prefetched fragments instead of whole windows (27–32 ms vs 22.9:
 // the band limit then rises too late), and windows at doubling stream lengths (28.0 vs 21.7 ms).
 constexpr int kFifo = kWindowGroups * 4;
-constexpr int kWarmChunks = FWAV_TOPK_WARM;   // ... and after every group during the first 64 chunks
+static_assert((kFifo & (kFifo - 1)) == 0, "the fired-chunk ring needs a power-of-two size");
+constexpr int kWarmChunks = FWAV_TOPK_WARM;   // ... and after every group during the first 32 chunks
 
 
 __device__ __forceinline__ float score32(const float* __restrict__ emb, int64_t d, const float (&q)[16]) {
