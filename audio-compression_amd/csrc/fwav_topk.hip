@@ -821,7 +821,7 @@ __device__ __forceinline__ float seed_limit(const _Float16* __restrict__ emb16, 
 // two halves of the workgroup, which otherwise reach their MFMA and fold phases in lockstep.
 template <int NC, int QS, int MODE = 0, int ROT = 0>
 __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, const half8 (&b)[QS],
-                                             const int (&thi)[QS], int64_t cbase, uint32_t (*fired)[kFifo],
+                                             const int (&thi)[QS], int cbase, uint32_t (*fired)[kFifo],
                                              int (&nfired)[QS], int lane, int* sink = nullptr) {
   constexpr int NT = 8 * NC;
   constexpr int kChunkHalfs = 512 * 8;  // one 8 KB chunk slot
@@ -977,19 +977,19 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
         gstats[16 + slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb)] = __float_as_uint(seed);
     }
   }
-  const int64_t nchunks = cdiv(nd, kChunk);
+  const int nchunks = (int)cdiv(nd, kChunk);  // < 2^31 / 256: chunk arithmetic stays 32-bit (scalar)
   // this item's chunk range [c0, c1) (the whole table unless the block is split)
-  const int64_t c0 = nchunks * piece / npieces, c1 = nchunks * (piece + 1) / npieces;
-  const int64_t ngroups = cdiv(c1 - c0, G);
+  const int c0 = (int)((int64_t)nchunks * piece / npieces), c1 = (int)((int64_t)nchunks * (piece + 1) / npieces);
+  const int ngroups = (c1 - c0 + G - 1) / G;
   const u32x4* src = reinterpret_cast<const u32x4*>(emb16);
   // Chunk stream: global → LDS directly (global_load_lds_dwordx4: no staging registers, no ds_write).  The
   // destination of one wave-instruction is wave-uniform base + lane × 16 B, which is exactly the slot layout
   // (thread t ↔ bytes [16t, 16t + 16) of the 8 KB chunk).  Chunks past the end re-read the last one (never
   // consumed).  Group g+1 is issued right after the barrier that retires group g and frees its half.
-  auto issue_group = [&](int64_t gg) {
+  auto issue_group = [&](int gg) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-      int64_t c_ = c0 + gg * G + j;
+      int c_ = c0 + gg * G + j;
       c_ = c_ < c1 ? c_ : c1 - 1;
       if (ABL && (dbg & 4)) c_ = 0;  // ablation: no streaming traffic beyond one L2-resident chunk
       if (ABL && (dbg & 128) && (j & 1)) continue;  // ablation: DMA only every other chunk
@@ -999,7 +999,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
         // of the other half; completion is counted by hand at the group top
         const unsigned lds_dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(
             (__attribute__((address_space(3))) void*)(&slots[(gg & 1) * G + j][k * 64])));
-        const u32x4* gsrc = src + c_ * 512 + k * 64 + lane;
+        const u32x4* gsrc = src + (int64_t)c_ * 512 + k * 64 + lane;
         unsigned keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
@@ -1041,7 +1041,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
         for (int k = wave; k < 8; k += Wact) {
           const unsigned lds_dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(
               (__attribute__((address_space(3))) void*)(&slots[(gg % NGS) * G + j][k * 64])));
-          const u32x4* gsrc = src + c_ * 512 + k * 64 + lane;
+          const u32x4* gsrc = src + (int64_t)c_ * 512 + k * 64 + lane;
           unsigned keep;
           asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                        : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
@@ -1114,10 +1114,10 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
     }
     publish();
   } else
-  for (int64_t g = 0; g < ngroups; ++g) {
+  for (int g = 0; g < ngroups; ++g) {
     u32x4(*half)[512] = slots + (g & 1) * G;
-    const int64_t cg = c0 + g * G;  // first chunk of group g
-    const int64_t c_end = cg + G < c1 ? cg + G : c1;
+    const int cg = c0 + g * G;  // first chunk of group g
+    const int c_end = cg + G < c1 ? cg + G : c1;
     const bool window_end =
         (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
     const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1160,7 +1160,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
         stream_group<G, QS>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
 #endif
     } else {
-      for (int64_t c = cg; c < c_end; ++c)
+      for (int c = cg; c < c_end; ++c)
         stream_group<1, QS>(lda0 + (c - cg) * 512 * 8, b, thi, c, sm.fired + wave * QS, nfired, lane);
     }
     const unsigned long long t_c = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
