@@ -55,18 +55,58 @@ def compress_audio(signal, framerate, sampwidth, tile_size=1024, emb_dim=16, top
     sig = np.asarray(signal, dtype=np.float32)
     rs, step = engine.geometry(tile_size)
     t = torch.from_numpy(np.ascontiguousarray(sig)).to(dev)
-    res = engine.compress_device(t, tile_size, k, energy_thresh=energy_thresh, fast_mode=fast_mode)
-    return device_result_to_tuple(res)
+    copy = _PoolCopy(dev)
+    res = engine.compress_device(t, tile_size, k, energy_thresh=energy_thresh, fast_mode=fast_mode,
+                                 on_pool=copy.start)
+    return device_result_to_tuple(res, copy)
 
 
-def device_result_to_tuple(res: "engine.DeviceCompressed"):
+_side_streams: dict = {}
+
+
+class _PoolCopy:
+    """Device→host copy of the domain pool on a side stream, started as soon as the pool kernel is queued so that it
+    overlaps the similarity search (the pool is the largest host output: nd × rs f32).  The destination is pinned
+    (torch's caching host allocator reuses it across calls) and is handed to the caller as a numpy view."""
+
+    def __init__(self, dev: torch.device):
+        self.dev, self.host, self.done = dev, None, None
+
+    def start(self, pool: torch.Tensor) -> None:
+        side = _side_streams.get(self.dev)
+        if side is None:
+            side = _side_streams[self.dev] = torch.cuda.Stream(self.dev)
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.dev))
+        self.host = torch.empty(pool.numel(), dtype=pool.dtype, pin_memory=True)
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            self.host.copy_(pool, non_blocking=True)
+            pool.record_stream(side)
+            self.done = torch.cuda.Event()
+            self.done.record(side)
+
+    def result(self) -> np.ndarray:
+        self.done.synchronize()
+        return self.host.numpy()
+
+
+def device_result_to_tuple(res: "engine.DeviceCompressed", pool_copy: "_PoolCopy | None" = None):
     rs, tile, step, thr, orig = res.range_size, res.tile_size, res.domain_step, res.energy_thresh, res.original_len
     empty = ([], np.zeros((0, rs), dtype=np.float32), 0, rs, tile, step, thr, orig)
     if res.empty or res.is_silent():
         return empty
-    matches = MatchList(res.idx.cpu().numpy(), res.s.cpu().numpy(), res.o.cpu().numpy(), res.sym.cpu().numpy(),
-                        res.err.cpu().numpy())
-    domains = res.pool.view(res.n_domains, rs).cpu().numpy()
+    # the five match arrays into pinned buffers, one synchronisation for all of them
+    src = (res.idx, res.s, res.o, res.sym, res.err)
+    hs = [torch.empty(t.numel(), dtype=t.dtype, pin_memory=True) for t in src]
+    for h, t in zip(hs, src):
+        h.copy_(t, non_blocking=True)
+    torch.cuda.current_stream(res.idx.device).synchronize()
+    matches = MatchList(*[h.numpy() for h in hs])
+    if pool_copy is not None and pool_copy.done is not None:
+        domains = pool_copy.result().reshape(res.n_domains, rs)
+    else:
+        domains = res.pool.view(res.n_domains, rs).cpu().numpy()
     return (matches, domains, res.n_ranges, rs, tile, step, thr, orig)
 
 

@@ -114,14 +114,15 @@ def _empty(n, rs, tile, step, thr, k) -> DeviceCompressed:
 def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh: float = 1e-4,
                     fast_mode: bool = True, s_clip: float = 16.0, shard: Optional[tuple[int, int]] = None,
                     keep_intermediates: bool = False, events: Optional[dict] = None,
-                    search: str = "f16") -> DeviceCompressed:
+                    search: str = "f16", on_pool=None) -> DeviceCompressed:
     """Run the compress hot path on ``sig`` (1-D float32 tensor on a HIP device).
 
     ``shard=(lo, hi)`` restricts candidate search and the affine solve to ranges ``[lo, hi)`` (the
     multi-GPU path); voiced detection, pool and embeddings are always computed for the whole signal,
     because query vectors are domain-embedding rows (quirk Q1) and the voiced state is a scan over the
     whole signal.  Raises ValueError for the reference's own error cases (empty input; n_ranges >
-    n_domains).
+    n_domains).  ``on_pool(pool)``, when given, is called right after the pool kernel is queued (the API
+    starts the pool's device→host copy there, on a side stream, so that it overlaps the search).
     """
     if sig.dim() != 1 or sig.dtype != torch.float32 or not sig.is_cuda:
         raise ValueError("compress_device expects a 1-D float32 device tensor")
@@ -177,6 +178,8 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
     call("fwav_pool_embed", sig.data_ptr(), n, tile_size, rs, step, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
          _p(emb16), wsp.data_ptr(), ws_p, st)
     _mark(events, "pool_embed")
+    if on_pool is not None:
+        on_pool(pool)
     m = hi - lo
     cand = torch.empty(max(m, 1) * k, dtype=torch.int32, device=dev)
     active = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
