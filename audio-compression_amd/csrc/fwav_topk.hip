@@ -294,6 +294,9 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_WPE
 #define FWAV_TOPK_WPE 4  // launch bound: waves per SIMD the register allocation must allow
 #endif
+#ifndef FWAV_TOPK_OVF_F32
+#define FWAV_TOPK_OVF_F32 0  // 1: recompute overflowed queries with the all-f32 kernel (the former path)
+#endif
 // Ablation builds (tools/ab_build.sh NAME -DFWAV_TOPK_ABL=<dbg bits>): the production kernel with the given `dbg`
 // bits fixed at compile time — the STATS kernel's counters cost registers (it spills), which skews its timings.
 #ifndef FWAV_TOPK_ABL
@@ -616,10 +619,44 @@ __device__ __forceinline__ int fold16(int r, const floatx16& a) {
 // One recomputed tile of a replay (acc = the tile's fp16 MFMA scores, domains dt .. dt+31): append the
 // survivors (s16 keys) to the wave-owned global key buffers — one LDS atomic per lane reserves the slots,
 // the stores are fire-and-forget — and compact a buffer inline only when it is about to overflow.
-template <int C, bool STATS, class SM>
+// Exact-mode compaction (the overflow relaunch, EX): the buffer holds exact f32 keys, so it keeps exactly its top K
+// (a sort of the ≤ C keys; entries are distinct (score, index) keys, so no tie group can overflow), written sorted at
+// the front.  New domains can only matter with s32 > S32_K (a later domain of equal score has a larger index), i.e.
+// s16 > S32_K − δ: that is the returned filter limit.
+template <int C>
+__device__ __forceinline__ void compact_exact(uint64_t* __restrict__ kq, int n0, int n1, int K, int& m_out,
+                                              float& lim_out, uint64_t& kth_out) {
+  constexpr int E = C / 64;
+  const int lane = threadIdx.x & 63;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int n = min(n0 + n1, C);
+  uint64_t v[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    v[j] = e < n ? ld_key(kq + two_end_slot<C>(e, n0)) : 0ull;
+  }
+  wave_sort_desc<E>(v);
+  const int kl = (K - 1) & 63, kj = (K - 1) >> 6;
+  uint64_t kth = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j)
+    if (j == kj) kth = __shfl(v[j], kl);
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    if (e < K && e < n) kq[e] = v[j];
+  }
+  m_out = n < K ? n : K;
+  lim_out = n >= K ? key_score(kth) - kF16Delta : -INFINITY;
+  kth_out = n >= K ? kth : 0ull;
+}
+
+template <int C, bool STATS, class SM, bool EX = false>
 __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int& qcnt, int& kept, int64_t dt, int64_t nd,
                                              uint64_t* __restrict__ gkeys, SM& sm, int qg, int K, int upd,
-                                             unsigned long long* stats) {
+                                             unsigned long long* stats, const float* __restrict__ emb = nullptr,
+                                             const float* qv = nullptr, uint64_t* kthp = nullptr) {
   const int lane = threadIdx.x & 63;
   const int col = lane & 31;
   const int h = lane >> 5;
@@ -642,16 +679,33 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
   int slot = h ? C - 1 - qcnt : qcnt;
   const int step = h ? -1 : 1;
   char* kbase = reinterpret_cast<char*>(gkeys);
+  // EX: the tile's exact f32 scores, by the f32 MFMA in the fixed k = 0..15 order (bitwise the fma chain of the
+  // final rescoring; the layout of `acc`): lane (col, h) feeds domain dt + col, dims 2s + h
+  floatx16 ex = {};
+  if constexpr (EX) {
+    const float* rp = emb + (dt + col < nd ? dt + col : nd - 1) * 16 + h;
+    float av[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) av[s] = rp[2 * s];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) ex = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], qv[2 * s + h], ex, 0, 0, 0);
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     if (a[r] > thf) {
       FWAV_TRACE(sm.qrow[ql], 1u, (uint32_t)dt, (uint32_t)((h << 16) | r), (uint32_t)slot);
-      // f2key, branch-free: negative → ~u, else u | sign
-      const uint32_t u = __float_as_uint(a[r]);
+      // f2key, branch-free: negative → ~u, else u | sign.  EX: the exact f32 score (fixed fma chain) instead of s16
+      float sc = a[r];
+      if constexpr (EX) sc = ex[r];
+      const uint32_t u = __float_as_uint(sc);
       const uint32_t key = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
-      *reinterpret_cast<uint64_t*>(kbase + (uint32_t)((ql * C + slot) * 8)) =
-          ((uint64_t)key << 32) | (uint64_t)(nd0 - (uint32_t)((r & 3) + 8 * (r >> 2)));
-      slot += step;
+      const uint64_t k64 = ((uint64_t)key << 32) | (uint64_t)(nd0 - (uint32_t)((r & 3) + 8 * (r >> 2)));
+      // EX: a domain that does not beat the query's current K-th exact key can never enter its top K (groups of
+      // equal scores — repeated or silent tiles — are decided here, without stores or compactions)
+      if (!EX || k64 > *kthp) {
+        *reinterpret_cast<uint64_t*>(kbase + (uint32_t)((ql * C + slot) * 8)) = k64;
+        slot += step;
+      }
     }
   }
   qcnt = h ? C - 1 - slot : slot;  // this lane's entries; ≤ C in total: see the compaction trigger below
@@ -670,12 +724,20 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
     need &= need - 1;
     int m;
     float lim;
-    compact16_s16<C>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l),
-                     __builtin_amdgcn_readlane(qcnt, l + 32), sm, qg * 32 + l, K, STATS ? stats : nullptr, m, lim);
+    uint64_t kth_l = 0;
+    if constexpr (EX)
+      compact_exact<C>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l),
+                       __builtin_amdgcn_readlane(qcnt, l + 32), K, m, lim, kth_l);
+    else
+      compact16_s16<C>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l),
+                       __builtin_amdgcn_readlane(qcnt, l + 32), sm, qg * 32 + l, K, STATS ? stats : nullptr, m, lim);
     if (col == l) {
       qcnt = h ? 0 : m;  // the kept band is written densely at the front
       kept = m;
       if (upd) thf = fmaxf(thf, lim);  // the seed may be above a buffer's own limit
+      // a query whose band overflowed is searched again in exact mode: stop appending for it here
+      if (!EX && sm.ovf[qg * 32 + l]) thf = INFINITY;
+      if (EX) *kthp = kth_l;
     }
   }
   return thf;
@@ -720,10 +782,12 @@ __device__ __forceinline__ half8 tile_fragment(const _Float16* __restrict__ emb1
   return *reinterpret_cast<const half8*>(emb16 + ((c * 2 + h) * kChunk + col) * 8 + t * 256);
 }
 
-template <int C, bool STATS, class SM>
+template <int C, bool STATS, class SM, bool EX = false>
 __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int& qcnt,
                                                int& kept, ReplayCursor& cur, int tail, int64_t nd, uint64_t* __restrict__ gkeys,
-                                               SM& sm, int qg, int K, int upd, unsigned long long* stats) {
+                                               SM& sm, int qg, int K, int upd, unsigned long long* stats,
+                                               const float* __restrict__ emb = nullptr, const float* qv = nullptr,
+                                               uint64_t* kthp = nullptr) {
   const int lane = threadIdx.x & 63;
   const int col = lane & 31;
   const int h = lane >> 5;
@@ -746,7 +810,8 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
     for (int u = 0; u < kReplayBatch; ++u) {
       if (ct[u] < 0) break;
       const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], b, floatx16{}, 0, 0, 0);
-      thf = append_tile<C, STATS>(acc, thf, qcnt, kept, ct[u], nd, gkeys, sm, qg, K, upd, stats);
+      thf = append_tile<C, STATS, SM, EX>(acc, thf, qcnt, kept, ct[u], nd, gkeys, sm, qg, K, upd, stats, emb, qv,
+                                          kthp);
     }
     if (ct[kReplayBatch - 1] < 0) break;
   }
@@ -883,7 +948,7 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
   }
 }
 
-template <int C, bool STATS, int W = k16Waves, int G = kGroup, int QS = k16Sets>
+template <int C, bool STATS, int W = k16Waves, int G = kGroup, int QS = k16Sets, bool EX = false>
 __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
                                                                 const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
@@ -940,6 +1005,8 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
   half8 b[QS];
   float thf[QS];
   int upd[QS];
+  float qv[QS][EX ? 16 : 1];  // EX: exact query vectors
+  uint64_t kth[QS];           // EX: the query's current K-th exact key (0 until K entries)
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     const int ql = (wave * QS + s) * 32 + col;
@@ -952,6 +1019,15 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
     if (h == 0) {
       sm.ovf[ql] = 0;
       sm.qrow[ql] = qrow;
+    }
+    kth[s] = 0ull;
+    if constexpr (EX) {  // the query's exact vector (both lanes of the query)
+      const float4* qp = reinterpret_cast<const float4*>(emb + qrow * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 w = qp[j];
+        qv[s][4 * j] = w.x; qv[s][4 * j + 1] = w.y; qv[s][4 * j + 2] = w.z; qv[s][4 * j + 3] = w.w;
+      }
     }
   }
 
@@ -1105,8 +1181,8 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
 #pragma unroll
         for (int s = 0; s < QS; ++s) {
           if (nfired[s] > cur[s].head || cur[s].rem != 0u)
-            thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], kept[s], cur[s], nfired[s], nd, gkeys, sm,
-                                             wave * QS + s, K, upd[s], stats);
+            thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, EX>(emb16, b[s], thf[s], qcnt[s], kept[s], cur[s],
+                                             nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s]);
         }
         if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
         __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -1170,8 +1246,8 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
         if (nfired[s] > cur[s].head || cur[s].rem != 0u)
-          thf[s] = replay_window<C, STATS>(emb16, b[s], thf[s], qcnt[s], kept[s], cur[s], nfired[s], nd, gkeys, sm,
-                                           wave * QS + s, K, upd[s], stats);
+          thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, EX>(emb16, b[s], thf[s], qcnt[s], kept[s], cur[s],
+                                           nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s]);
       }
       if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
       // retire the replay's loads and stores here, visibly to hipcc's wait bookkeeping (vmcnt(0) expcnt(7)
@@ -1363,7 +1439,11 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     if (pl.R > 0)
       k_merge_pieces<k16Cap><<<cdiv(pl.R * k16QB, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, ovf_list,
                                                                     n_ovf);
-    // queries whose fp16 band overflowed the buffer (none for ordinary audio): exact f32 recompute
+    // Queries whose fp16 band overflowed the buffer (large groups of near-equal scores: periodic or speech-like
+    // signals) are searched again by the same kernel in exact mode: appends carry exact f32 keys and a compaction
+    // keeps exactly the top K, so nothing can overflow.  The relaunch reads its query list and count from the
+    // overflow list on the device (no host sync) and exits at once when it is empty.
+#if FWAV_TOPK_OVF_F32
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32b = false;
     if (!attr32b) {
@@ -1371,6 +1451,11 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       attr32b = true;
     }
     k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, ovf_list, n_ovf, q_offset, K, cand);
+#else
+    const TopkPlan pl_ex = make_plan(max_q, 0, 1);
+    k_sim_topk_f16<k16Cap, false, k16Waves, kGroup, k16Sets, true><<<pl_ex.items(), 64 * k16Waves, 0, st>>>(
+        emb16, emb, nd, ovf_list, n_ovf, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, 1, 0, nullptr);
+#endif
   } else {
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32 = false;

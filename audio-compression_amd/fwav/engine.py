@@ -207,7 +207,7 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
         _mark(events, "affine")
     res.pool, res.idx, res.s, res.o, res.sym, res.err, res.n_active = pool, idx, s, o, sym, err, n_active
     if keep_intermediates:
-        res.ranges, res.emb, res.cand = ranges, emb, cand
+        res.ranges, res.emb, res.cand, res.active = ranges, emb, cand, active
     return res
 
 

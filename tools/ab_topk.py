@@ -21,32 +21,41 @@ for path in sys.argv[1:]:
     res, args = SIGNATURES["fwav_sim_topk"]
     L.fwav_sim_topk.restype, L.fwav_sim_topk.argtypes = res, args
     libs.append((os.path.basename(path), L))
-sig = torch.from_numpy(synth.noise(60.0, 44100)).cuda()
-r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
+cfg = os.environ.get("AB_CFG", "cfg2")  # cfg3: the speech-like 10 min case (its pruned active list)
+sig_h, _, _ = synth.make_config_signal(cfg)
+tile = synth.CONFIGS[cfg]["tile"]
+sig = torch.from_numpy(sig_h).cuda()
+r = engine.compress_device(sig, tile, 64, keep_intermediates=True)
 torch.cuda.synchronize()
 nd, nr = r.n_domains, r.n_ranges
+rs, step = engine.geometry(tile)
 emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 from fwav._lib import call  # noqa: E402
-tab = engine.embed_tables(8, torch.device("cuda"))
-pool = torch.empty(nd * 8, device="cuda")
+tab = engine.embed_tables(rs, torch.device("cuda"))
+pool = torch.empty(nd * rs, device="cuda")
 emb = torch.empty(nd * 16, device="cuda")
-ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
+wsp = size_call("fwav_pool_workspace_size", sig.numel(), tile, rs, step)
+ws = torch.empty(max(wsp, 16), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
-call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
+call("fwav_pool_embed", sig.data_ptr(), sig.numel(), tile, rs, step, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
      emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
-nq = int(os.environ.get("AB_NQ", nr))  # active queries (default: all ranges)
-active = torch.arange(nq, dtype=torch.int32, device="cuda")
+if cfg == "cfg2":
+    nq = int(os.environ.get("AB_NQ", nr))  # active queries (default: all ranges)
+    active = torch.arange(nq, dtype=torch.int32, device="cuda")
+else:  # the engine's own pruned active list
+    nq = int(r.n_active.item())
+    active = r.active[:nq].clone() if hasattr(r, "active") else torch.arange(nq, dtype=torch.int32, device="cuda")
 n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
 # each build's plan (and so its workspace) depends on its own occupancy: size for the largest
 wsn = 0
 for _, L in libs:
     L.fwav_sim_topk_workspace_size.restype = C.c_size_t
     L.fwav_sim_topk_workspace_size.argtypes = [C.c_int64, C.c_int64, C.c_int]
-    wsn = max(wsn, L.fwav_sim_topk_workspace_size(nr, nd, 64))
+    wsn = max(wsn, L.fwav_sim_topk_workspace_size(nq, nd, 64))
 wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
 outs = {}
 times = {n: [] for n, _ in libs}
-for rnd in range(4):
+for rnd in range(int(os.environ.get("AB_ROUNDS", 4))):
     for name, L in libs:
         cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
         e0 = torch.cuda.Event(enable_timing=True)
