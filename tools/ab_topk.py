@@ -69,6 +69,10 @@ for rnd in range(int(os.environ.get("AB_ROUNDS", 4))):
         if rnd > 0:
             times[name].append(e0.elapsed_time(e1))
         outs[name] = cand
+        if rnd == 0:  # overflowed queries of this build: the i32 count at the end of its own workspace layout
+            own = L.fwav_sim_topk_workspace_size(nq, nd, 64)
+            n_ovf = int(wsk[own - 4:own].view(torch.int32).item())
+            print(f"{name:24s} active {nq}  overflowed {n_ovf} ({100.0 * n_ovf / max(nq, 1):.1f}%)", flush=True)
 ref = outs[libs[0][0]]
 for name, _ in libs:
     same = bool(torch.equal(outs[name], ref))

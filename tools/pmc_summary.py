@@ -24,6 +24,8 @@ def per_kernel(d, counter):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
+    # gpurun merges each call's gpurun_out/ into the local one, so older passes may lie beside this one: newest only
+    files = [max(files, key=os.path.getmtime)]
     for f in files:
         with open(f, newline="") as fh:
             for row in csv.DictReader(fh):
