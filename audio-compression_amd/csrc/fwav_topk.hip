@@ -313,6 +313,11 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 // STAGGER: 1 = the second half of the waves takes each group's chunks in rotated order, 2 = every wave of a SIMD
 // pair starts on a different chunk.  Neutral in same-box A/B (21.73 / 21.76 / 22.00 ms for 0 / 1 / 2); a static
 // s_setprio for the second half was slower (+3 %).
+// Exact mode (overflow relaunch) compacts every FWAV_TOPK_EXGROW appends, so its K-th exact key — the store filter —
+// and band limit rise sooner (cfg3: 32 / 64 / 96 / 128 / full buffer 859 / 861 / 870 / 887 / 898 ms)
+#ifndef FWAV_TOPK_EXGROW
+#define FWAV_TOPK_EXGROW 64
+#endif
 #ifndef FWAV_TOPK_STAGGER
 #define FWAV_TOPK_STAGGER 0
 #endif
@@ -683,8 +688,9 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
   // final rescoring; the layout of `acc`): lane (col, h) feeds domain dt + col, dims 2s + h
   floatx16 ex = {};
   if constexpr (EX) {
-    const float* rp = emb + (dt + col < nd ? dt + col : nd - 1) * 16 + h;
+    // (4 float4 loads of the whole row + selects: 916 vs 894 ms at cfg3)
     float av[8];
+    const float* rp = emb + (dt + col < nd ? dt + col : nd - 1) * 16 + h;
 #pragma unroll
     for (int s = 0; s < 8; ++s) av[s] = rp[2 * s];
 #pragma unroll
@@ -718,7 +724,8 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
   }
   // compact when fewer than 32 free slots remain (a tile adds ≤ 16 per lane, ≤ 32 per query) — or, to raise the band
   // limit sooner, once the buffer passes kTrig and has grown by kGrow since its last compaction
-  uint64_t need = __ballot(lane < 32 && (total > C - 32 || (total > kTrig && total >= kept + kGrow)));
+  uint64_t need = __ballot(lane < 32 && (total > C - 32 || (total > kTrig && total >= kept + kGrow) ||
+                                         (EX && FWAV_TOPK_EXGROW > 0 && total >= kept + FWAV_TOPK_EXGROW)));
   while (need != 0ull) {
     const int l = __builtin_ctzll(need);
     need &= need - 1;
@@ -1430,7 +1437,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
           emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, 0, stats);
     else
 #endif
-    if (stats != nullptr || (dbg & 65535) != 0)
+    if ((stats != nullptr && !(dbg & (1 << 17))) || (dbg & 65535) != 0)
       k_sim_topk_f16<k16Cap, true><<<pl.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, dbg & 65535, stats);
     else
@@ -1453,8 +1460,12 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, ovf_list, n_ovf, q_offset, K, cand);
 #else
     const TopkPlan pl_ex = make_plan(max_q, 0, 1);
-    k_sim_topk_f16<k16Cap, false, k16Waves, kGroup, k16Sets, true><<<pl_ex.items(), 64 * k16Waves, 0, st>>>(
-        emb16, emb, nd, ovf_list, n_ovf, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, 1, 0, nullptr);
+    if (stats != nullptr && (dbg & (1 << 17)))  // diagnostic: counters of the exact-mode relaunch only
+      k_sim_topk_f16<k16Cap, true, k16Waves, kGroup, k16Sets, true><<<pl_ex.items(), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, ovf_list, n_ovf, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, 1, 0, stats);
+    else
+      k_sim_topk_f16<k16Cap, false, k16Waves, kGroup, k16Sets, true><<<pl_ex.items(), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, ovf_list, n_ovf, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, 1, 0, nullptr);
 #endif
   } else {
     const size_t lds = topk_lds_bytes<C>();

@@ -1,0 +1,56 @@
+"""Counters of the exact-mode relaunch of the fp16 search (overflowed queries) on cfg3 (tools only).
+usage: python tools/ex_stats.py"""
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd")]
+import torch
+
+import __graft_entry__
+
+__graft_entry__.build()
+from fwav import engine, synth  # noqa: E402
+from fwav._lib import call, size_call  # noqa: E402
+
+cfg = os.environ.get("AB_CFG", "cfg3")
+sig_h, _, _ = synth.make_config_signal(cfg)
+tile = synth.CONFIGS[cfg]["tile"]
+sig = torch.from_numpy(sig_h).cuda()
+r = engine.compress_device(sig, tile, 64, keep_intermediates=True)
+torch.cuda.synchronize()
+nd, nr = r.n_domains, r.n_ranges
+rs, step = engine.geometry(tile)
+st = torch.cuda.current_stream().cuda_stream
+emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+tab = engine.embed_tables(rs, torch.device("cuda"))
+pool = torch.empty(nd * rs, device="cuda")
+emb = torch.empty(nd * 16, device="cuda")
+ws = torch.empty(max(size_call("fwav_pool_workspace_size", sig.numel(), tile, rs, step), 16), dtype=torch.uint8,
+                 device="cuda")
+call("fwav_pool_embed", sig.data_ptr(), sig.numel(), tile, rs, step, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
+     emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+nq = int(r.n_active.item())
+active = r.active[:nq].clone()
+n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
+wsn = size_call("fwav_sim_topk_workspace_size", nq, nd, 64)
+wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
+cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
+stats = torch.zeros(16, dtype=torch.int64, device="cuda")
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0, 64,
+     cand.data_ptr(), wsk.data_ptr(), 1 << 17, stats.data_ptr(), st)
+e1.record()
+torch.cuda.synchronize()
+n_ovf = int(wsk[wsn - 4:wsn].view(torch.int32).item())
+sv = stats.cpu().tolist()
+qsets = max((n_ovf + 31) // 32, 1)
+tot = max(sv[6], 1)
+print(f"{cfg}: active {nq}, overflowed {n_ovf}; search incl. STATS relaunch {e0.elapsed_time(e1):.1f} ms")
+print("relaunch per query set of 32: replayed chunks %.0f, firing tiles %.0f; per query: appends %.1f, compactions "
+      "%.2f; wave time %.2f ms" % (sv[0] / qsets, sv[1] / qsets, sv[2] / max(n_ovf, 1), sv[3] / max(n_ovf, 1),
+                                   sv[6] / qsets / 1e5))
+print("shares: barrier %.3f, streaming %.3f, replays %.3f (compactions %.3f, appends %.3f, fragment loads %.3f), "
+      "final %.3f" % (sv[7] / tot, sv[9] / tot, sv[4] / tot, sv[5] / tot, sv[10] / tot, sv[11] / tot, sv[8] / tot),
+      flush=True)
