@@ -87,8 +87,9 @@ size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k);
 int fwav_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
                   const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand, void* workspace,
                   size_t ws_bytes, void* stream);
-/* Diagnostic ablations of the fp16 kernel (timing only, outputs invalid for dbg != 0); stats (u64[8] device,
- * may be NULL) receives slow-path counters.  Not used by the product path. */
+/* Diagnostic ablations of the fp16 kernel (timing only, outputs invalid for dbg & 65535 != 0); stats (u64[16]
+ * device, may be NULL) receives slow-path counters — of the first pass, or with dbg = 1 << 17 of the exact-mode
+ * relaunch for overflowed queries only (outputs valid).  Not used by the product path. */
 int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
                         const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand,
                         void* workspace, int dbg, unsigned long long* stats, void* stream);
