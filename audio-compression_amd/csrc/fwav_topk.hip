@@ -452,7 +452,7 @@ template <int NG, bool STATS>
 struct Topk16SmemT {
   int cnt[32 * NG];   // final pass: entries at the front of the query's buffer (its h = 0 lane's appends)
   int cnt1[32 * NG];  // ... and at the back (its h = 1 lane's)
-  int ovf[32 * NG];  // band overflowed the buffer: recompute this query with the f32 kernel
+  int ovf[32 * NG];  // band overflowed the buffer (f2key of its band limit, else 0): recompute in exact mode
   int64_t qrow[32 * NG];
   uint32_t fired[NG][kFifo];                       // deferred work: ring of fired chunk entries
   unsigned long long wstat[STATS ? NG : 1][kStats];  // STATS builds only (one row per wave)
@@ -520,7 +520,9 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0,
     m = C - 64;
     ovf = 1;
   }
-  if (lane == 0 && ovf) sm.ovf[ql] = 1;
+  // the flag carries the band limit at overflow (f2key, never 0): a valid lower bound on the s16 of every domain of
+  // the query's exact top K, so it seeds the exact-mode relaunch
+  if (lane == 0 && ovf) sm.ovf[ql] = (int)f2key(lim);
   if (lane == 0) FWAV_TRACE(sm.qrow[ql], 2u, (uint32_t)n, __float_as_uint(lim), (uint32_t)((ovf << 16) | m));
   m_out = m;
   lim_out = lim;
@@ -1014,6 +1016,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
   int upd[QS];
   float qv[QS][EX ? 16 : 1];  // EX: exact query vectors
   uint64_t kth[QS];           // EX: the query's current K-th exact key (0 until K entries)
+  float exseed[QS];           // EX: the first pass's band limit at overflow
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     const int ql = (wave * QS + s) * 32 + col;
@@ -1028,6 +1031,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       sm.qrow[ql] = qrow;
     }
     kth[s] = 0ull;
+    exseed[s] = EX && q >= 0 ? key2f(reinterpret_cast<const uint32_t*>(n_ovf + 1)[q]) : -INFINITY;
     if constexpr (EX) {  // the query's exact vector (both lanes of the query)
       const float4* qp = reinterpret_cast<const float4*>(emb + qrow * 16);
 #pragma unroll
@@ -1059,6 +1063,11 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       if (STATS && (dbg & 32768) && gstats != nullptr && h == 0 && upd[s])  // diagnostics: the seeds
         gstats[16 + slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb)] = __float_as_uint(seed);
     }
+  }
+  if constexpr (EX) {
+#pragma unroll
+    for (int s = 0; s < QS; ++s)
+      if (upd[s]) thf[s] = fmaxf(thf[s], exseed[s]);
   }
   const int nchunks = (int)cdiv(nd, kChunk);  // < 2^31 / 256: chunk arithmetic stays 32-bit (scalar)
   // this item's chunk range [c0, c1) (the whole table unless the block is split)
@@ -1280,6 +1289,8 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
     const int32_t qid = active[qq];
     uint64_t* kq = gkeys + (size_t)qs * C;
     if (lane == 0) FWAV_TRACE(sm.qrow[qs], 3u, (uint32_t)sm.cnt[qs], (uint32_t)sm.ovf[qs], (uint32_t)sm.cnt1[qs]);
+    // overflowed: the band limit seeds the exact-mode relaunch (max over the pieces of a split block)
+    if (lane == 0 && sm.ovf[qs]) atomicMax(reinterpret_cast<uint32_t*>(n_ovf + 1) + qid, (uint32_t)sm.ovf[qs]);
     // exact f32 rescoring of the kept band + sort; a piece keeps its top K in the buffer, the overflow flag in the
     // last entry (k_merge_pieces combines the block's pieces)
     compact16<C>(kq, sm, qs, K, emb, npieces == 1 ? cand + (int64_t)qid * K : nullptr);
@@ -1424,8 +1435,9 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     }
     const size_t keys_bytes = f16_keys_bytes(max_q, nd);
     int32_t* ovf_list = (int32_t*)((char*)gkeys + keys_bytes);
+    // workspace tail: ovf_list[q], n_ovf, then the overflow seeds u32[q] (f2key of band limits, 0 = none)
     int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
-    (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
+    (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t) * (1 + (max_q > 0 ? max_q : 1)), st);
     // Geometry: k16Waves waves × k16Sets query sets of 32 per workgroup.  Measured at cfg2 (W, QS=1): W = 8
     // 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms — an even 4 waves per SIMD beats a fuller last round of workgroups.
     int rt, P;
@@ -1499,7 +1511,7 @@ int fwav_topk_max_k(void) { return 4096; }
 size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   const int64_t q = max_q > 0 ? max_q : 1;
   if (k > 64) return large_workspace_bytes(n_domains, q);
-  return f16_keys_bytes(q, n_domains) + (size_t)(q + 1) * sizeof(int32_t);
+  return f16_keys_bytes(q, n_domains) + (size_t)(2 * q + 1) * sizeof(int32_t);
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,

@@ -71,7 +71,8 @@ for rnd in range(int(os.environ.get("AB_ROUNDS", 4))):
         outs[name] = cand
         if rnd == 0:  # overflowed queries of this build: the i32 count at the end of its own workspace layout
             own = L.fwav_sim_topk_workspace_size(nq, nd, 64)
-            n_ovf = int(wsk[own - 4:own].view(torch.int32).item())
+            o = own - 4 - 4 * max(nq, 1)  # ovf list, count, then u32 seeds[q]
+            n_ovf = int(wsk[o:o + 4].view(torch.int32).item())
             print(f"{name:24s} active {nq}  overflowed {n_ovf} ({100.0 * n_ovf / max(nq, 1):.1f}%)", flush=True)
 ref = outs[libs[0][0]]
 for name, _ in libs:

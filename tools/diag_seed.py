@@ -59,8 +59,9 @@ for plan in [(0, 1), (-1, 1)]:
         c = cand.cpu().numpy().reshape(-1, K)
         bad = np.nonzero(~np.all(c == ref, axis=1))[0]
         wb = wsk.cpu().numpy()
-        n_ovf = int(wb[wsn - 4:wsn].view(np.int32)[0])
-        ovf = wb[wsn - 4 - 4 * nr:wsn - 4].view(np.int32)[:n_ovf]
+        o = wsn - 4 - 4 * nr  # ovf list, its count, then u32 seeds[q]
+        n_ovf = int(wb[o:o + 4].view(np.int32)[0])
+        ovf = wb[o - 4 * nr:o].view(np.int32)[:n_ovf]
         print(f"   n_ovf {n_ovf}: bad rows in ovf list: {np.isin(bad, ovf).sum()} of {len(bad)}; ovf[:12] {np.sort(ovf)[:12]}")
         print(f"plan {plan} dbg {dbg}: {len(bad)} rows differ from f32", bad[:10])
         for q in bad[:3]:

@@ -43,7 +43,8 @@ call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_pt
      cand.data_ptr(), wsk.data_ptr(), 1 << 17, stats.data_ptr(), st)
 e1.record()
 torch.cuda.synchronize()
-n_ovf = int(wsk[wsn - 4:wsn].view(torch.int32).item())
+o = wsn - 4 - 4 * max(nq, 1)  # workspace tail: ovf list, its count, then u32 seeds[q]
+n_ovf = int(wsk[o:o + 4].view(torch.int32).item())
 sv = stats.cpu().tolist()
 qsets = max((n_ovf + 31) // 32, 1)
 tot = max(sv[6], 1)

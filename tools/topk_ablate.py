@@ -53,7 +53,8 @@ for dbg in (1, 4):
     torch.cuda.synchronize()
     sv = stats.cpu().tolist()
     tot = sv[6]
-    n_ovf = int(wsk[wsk.numel() - 4:].view(torch.int32).item())  # workspace tail: ovf list, then its count
+    o = wsk.numel() - 4 - 4 * nr  # workspace tail: ovf list, its count, then u32 seeds[q]
+    n_ovf = int(wsk[o:o + 4].view(torch.int32).item())
     print("dbg=%d: overflowed queries (f32 recompute) %d" % (dbg, n_ovf))
     print("dbg=%d: replays/wave %.0f firing tiles/wave %.0f appends/q %.0f compactions/q %.2f | shares: barrier %.3f, "
           "streaming %.3f, replays %.3f, final %.3f, other %.3f" %
