@@ -159,7 +159,8 @@ def test_f16_prefilter_equals_f32_larger(gen, tile, K):
 
 def test_f16_band_overflow_falls_back_to_exact():
     """A signal with a 32-sample period makes every domain have ~nd/32 exact duplicates: the fp16 band
-    overflows the key buffer, those queries are recomputed by the f32 kernel — results must stay identical."""
+    overflows the key buffer, those queries are searched again in exact mode (seeded with the first pass's band
+    limit) — results must stay identical to the all-f32 kernel."""
     n = 24000
     t = np.arange(n)
     sig = np.round(8000 * np.sin(2 * np.pi * t / 32) + 3000 * np.sin(2 * np.pi * 3 * t / 32)).astype(np.float32)
@@ -215,7 +216,7 @@ def test_f16_split_plans_equal_f32(plan):
     call("fwav_debug_topk_plan", *plan)
     try:
         a, _ = _cands(sig, 2048, 64, "f16")
-        p, _ = _cands(_periodic(), 1024, 32, "f16")  # band overflow inside pieces → f32 recompute after the merge
+        p, _ = _cands(_periodic(), 1024, 32, "f16")  # band overflow inside pieces → exact-mode relaunch after the merge
     finally:
         call("fwav_debug_topk_plan", -1, 1)
     assert np.array_equal(a, b)
