@@ -4,7 +4,7 @@ search (the oracle's scalar top-K would take hours at these sizes):
 * cfg3 (10 min speech-like @ 44.1 kHz, tile 4096: 1,653,750 ranges × 6,613,977 domains), the whole compress:
   voiced mask + ranges bit-exact vs the oracle over the whole signal; pool/embedding rows at the start, middle and
   end; the energy prune vs host energies; sampled queries' candidates are a top-K set of the exact scores (torch
-  fp32 rescoring, ties within 1e-5) and equal the all-f32 kernel's; affine bit-exact (oracle) on the sampled
+  fp32 rescoring, ties within 1e-5) and equal the all-f32 kernel's, as does every active query's candidate row; affine bit-exact (oracle) on the sampled
   ranges; decode bit-exact (oracle) over all ranges.
 * cfg4 (60 min @ 48 kHz, tile 2048: 86,398,977 domains — a 2.76 GB fp16 table, so table offsets pass 2^31): pool and
   embeddings at the end of the table, and a 2,048-range shard searched against the whole table (top-K property,
@@ -105,6 +105,18 @@ def test_cfg3_prune_and_search(cfg3):
     for r, c in zip(rows, got):
         check_topk_property(emb_t, int(r), c, K)
     assert np.array_equal(f32_search(res, rows, K), got)
+
+
+def test_cfg3_f16_equals_f32_every_query(cfg3):
+    """The whole cfg3 search (666,606 active queries; ≈ 35% overflow the fp16 band and take the exact-mode
+    relaunch) returns exactly the all-f32 kernel's candidates for every query."""
+    sig, res = cfg3
+    cand = res.cand.view(-1, K)
+    rows = np.nonzero(cand[:, 0].cpu().numpy() >= 0)[0]
+    assert len(rows) == int(res.n_active.item())
+    ref = f32_search(res, rows, K)
+    got = cand[torch.from_numpy(rows).to(dev())].cpu().numpy()
+    assert np.array_equal(ref, got), int((ref != got).any(axis=1).sum())
 
 
 def test_cfg3_affine_sampled(cfg3):
