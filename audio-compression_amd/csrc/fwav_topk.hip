@@ -315,6 +315,9 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 // s_setprio for the second half was slower (+3 %).
 // Exact mode (overflow relaunch) compacts every FWAV_TOPK_EXGROW appends, so its K-th exact key — the store filter —
 // and band limit rise sooner (cfg3: 32 / 64 / 96 / 128 / full buffer 859 / 861 / 870 / 887 / 898 ms)
+#ifndef FWAV_TOPK_EXWPE
+#define FWAV_TOPK_EXWPE 4
+#endif
 #ifndef FWAV_TOPK_EXGROW
 #define FWAV_TOPK_EXGROW 64
 #endif
@@ -696,7 +699,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
 #pragma unroll
     for (int s = 0; s < 8; ++s) av[s] = rp[2 * s];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) ex = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], qv[2 * s + h], ex, 0, 0, 0);
+    for (int s = 0; s < 8; ++s) ex = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], qv[s], ex, 0, 0, 0);
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -958,7 +961,7 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
 }
 
 template <int C, bool STATS, int W = k16Waves, int G = kGroup, int QS = k16Sets, bool EX = false>
-__global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
+__global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
                                                                 const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
                                                                 const int32_t* __restrict__ n_active_p,
@@ -1014,7 +1017,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
   half8 b[QS];
   float thf[QS];
   int upd[QS];
-  float qv[QS][EX ? 16 : 1];  // EX: exact query vectors
+  float qv[QS][EX ? 8 : 1];  // EX: this lane's half of the exact query vector, qv[s][i] = q[2i + h]
   uint64_t kth[QS];           // EX: the query's current K-th exact key (0 until K entries)
   float exseed[QS];           // EX: the first pass's band limit at overflow
 #pragma unroll
@@ -1031,14 +1034,12 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
       sm.qrow[ql] = qrow;
     }
     kth[s] = 0ull;
-    exseed[s] = EX && q >= 0 ? key2f(reinterpret_cast<const uint32_t*>(n_ovf + 1)[q]) : -INFINITY;
-    if constexpr (EX) {  // the query's exact vector (both lanes of the query)
-      const float4* qp = reinterpret_cast<const float4*>(emb + qrow * 16);
+    // EX: active = the overflow list, whose position qi holds this query's seed
+    exseed[s] = EX && q >= 0 ? key2f(reinterpret_cast<const uint32_t*>(n_ovf + 1)[qi]) : -INFINITY;
+    if constexpr (EX) {  // the f32 MFMA's B operand: dims 2i + h of the query
+      const float* qp = emb + qrow * 16 + h;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 w = qp[j];
-        qv[s][4 * j] = w.x; qv[s][4 * j + 1] = w.y; qv[s][4 * j + 2] = w.z; qv[s][4 * j + 3] = w.w;
-      }
+      for (int i = 0; i < 8; ++i) qv[s][i] = qp[2 * i];
     }
   }
 
@@ -1289,15 +1290,18 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
     const int32_t qid = active[qq];
     uint64_t* kq = gkeys + (size_t)qs * C;
     if (lane == 0) FWAV_TRACE(sm.qrow[qs], 3u, (uint32_t)sm.cnt[qs], (uint32_t)sm.ovf[qs], (uint32_t)sm.cnt1[qs]);
-    // overflowed: the band limit seeds the exact-mode relaunch (max over the pieces of a split block)
-    if (lane == 0 && sm.ovf[qs]) atomicMax(reinterpret_cast<uint32_t*>(n_ovf + 1) + qid, (uint32_t)sm.ovf[qs]);
     // exact f32 rescoring of the kept band + sort; a piece keeps its top K in the buffer, the overflow flag in the
     // last entry (k_merge_pieces combines the block's pieces)
     compact16<C>(kq, sm, qs, K, emb, npieces == 1 ? cand + (int64_t)qid * K : nullptr);
+    // overflowed: listed for the exact-mode relaunch with its band limit as the seed (same list position)
     if (npieces == 1) {
-      if (lane == 0 && sm.ovf[qs]) ovf_list[atomicAdd(n_ovf, 1)] = qid;
+      if (lane == 0 && sm.ovf[qs]) {
+        const int pos = atomicAdd(n_ovf, 1);
+        ovf_list[pos] = qid;
+        reinterpret_cast<uint32_t*>(n_ovf + 1)[pos] = (uint32_t)sm.ovf[qs];
+      }
     } else if (lane == 0) {
-      kq[C - 1] = sm.ovf[qs] ? 1ull : 0ull;
+      kq[C - 1] = (uint64_t)(uint32_t)sm.ovf[qs];  // 0, or the flag's band-limit key
     }
   }
   if (ABL && sink == 0x7fffffff) cand[0] = sink;
@@ -1315,7 +1319,7 @@ __global__ __launch_bounds__(64 * W, FWAV_TOPK_WPE) void k_sim_topk_f16(const _F
 
 // Merge the pieces of split blocks: per query, the P sorted exact top-K key lists of its block's pieces → the
 // top K of their union (the top K of a union is the top K of the parts' top Ks), ties by index as everywhere.
-// One wave per query; a query flagged by any piece goes to the f32 recompute list once.
+// One wave per query; a query flagged by any piece goes to the exact-mode relaunch list once, with the largest seed.
 template <int C>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
@@ -1334,7 +1338,7 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   if (qq >= n_active) return;
   const int P = plan.P;
   uint64_t v[E];
-  int flag = 0;
+  uint32_t seed = 0u;  // overflow: max over the pieces of their band-limit keys (each a valid lower bound); 0 = none
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     // slot j·64 + lane ↔ piece (j·64 + lane) / K, entry (j·64 + lane) % K
@@ -1345,9 +1349,11 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
       const int64_t item = plan.F + (block - plan.F) * P + p;
       const uint64_t* kq = gkeys_all + ((size_t)item * k16QB + ql) * C;
       v[j] = kq[r];
-      if (r == 0) flag |= kq[C - 1] != 0ull;
+      if (r == 0) seed = max(seed, (uint32_t)kq[C - 1]);
     }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) seed = max(seed, (uint32_t)__shfl_xor((int)seed, o));
   wave_sort_desc<E>(v);
   const int32_t qid = active[qq];
   int32_t* out = cand + (int64_t)qid * K;
@@ -1356,7 +1362,11 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
     const int e = j * 64 + lane;
     if (e < K) out[e] = v[j] != 0ull ? key_idx(v[j]) : -1;
   }
-  if (__ballot(flag) != 0ull && lane == 0) ovf_list[atomicAdd(n_ovf, 1)] = qid;
+  if (seed != 0u && lane == 0) {
+    const int pos = atomicAdd(n_ovf, 1);
+    ovf_list[pos] = qid;
+    reinterpret_cast<uint32_t*>(n_ovf + 1)[pos] = seed;
+  }
 }
 
 // Host-side plan: default policy from the device's workgroup slots, or a diagnostic override.
@@ -1435,9 +1445,9 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     }
     const size_t keys_bytes = f16_keys_bytes(max_q, nd);
     int32_t* ovf_list = (int32_t*)((char*)gkeys + keys_bytes);
-    // workspace tail: ovf_list[q], n_ovf, then the overflow seeds u32[q] (f2key of band limits, 0 = none)
+    // workspace tail: ovf_list[q], n_ovf, then seeds u32[q] (seeds[i] = f2key of the band limit of ovf_list[i])
     int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
-    (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t) * (1 + (max_q > 0 ? max_q : 1)), st);
+    (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
     // Geometry: k16Waves waves × k16Sets query sets of 32 per workgroup.  Measured at cfg2 (W, QS=1): W = 8
     // 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms — an even 4 waves per SIMD beats a fuller last round of workgroups.
     int rt, P;

@@ -222,3 +222,43 @@ def test_f16_split_plans_equal_f32(plan):
     assert np.array_equal(a, b)
     q, _ = _cands(_periodic(), 1024, 32, "f32")
     assert np.array_equal(p, q)
+
+
+def test_overflow_with_sparse_active_list():
+    """max_q bounds the number of listed queries, not their indices: a short active list of large local indices on a
+    signal whose fp16 bands overflow must keep the overflow bookkeeping inside the workspace (guard bytes after it
+    stay untouched) and return the all-f32 kernel's candidates."""
+    from fwav import engine as E
+    from fwav._lib import size_call
+    sig = td(_periodic())
+    tile, K = 1024, 32
+    rs, step = E.geometry(tile)
+    nd = (sig.numel() - tile) // step + 1
+    st = torch.cuda.current_stream().cuda_stream
+    tab = E.embed_tables(rs, sig.device)
+    pool = torch.empty(nd * rs, device=sig.device)
+    emb = torch.empty(nd * 16, device=sig.device)
+    emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device=sig.device)
+    ws = torch.empty(max(size_call("fwav_pool_workspace_size", sig.numel(), tile, rs, step), 16), dtype=torch.uint8,
+                     device=sig.device)
+    call("fwav_pool_embed", sig.data_ptr(), sig.numel(), tile, rs, step, tab.data_ptr(), pool.data_ptr(),
+         emb.data_ptr(), emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+    n = nd // 2                                     # local queries 0 .. n−1 have cand rows
+    rows = torch.arange(n - 300, n, dtype=torch.int32, device=sig.device)  # indices far above max_q
+    max_q = len(rows)
+    n_act = torch.tensor([max_q], dtype=torch.int32, device=sig.device)
+    out = []
+    for e16 in (emb16.data_ptr(), None):
+        wsn = size_call("fwav_sim_topk_workspace_size", max_q, nd, K)
+        guard = 1 << 20
+        wsk = torch.zeros(wsn + guard, dtype=torch.uint8, device=sig.device)
+        cand = torch.full((n * K,), -7, dtype=torch.int32, device=sig.device)
+        call("fwav_sim_topk", emb.data_ptr(), e16, nd, rows.data_ptr(), n_act.data_ptr(), max_q, 0, K,
+             cand.data_ptr(), wsk.data_ptr(), wsn, st)
+        torch.cuda.synchronize()
+        assert int(wsk[wsn:].count_nonzero().item()) == 0, "write past the workspace"
+        out.append(cand.view(n, K)[rows.long()].cpu().numpy())
+        if e16 is not None:  # workspace tail: ovf list, its count, seeds — the exact-mode path must have run
+            o = wsn - 4 - 4 * max_q
+            assert int(wsk[o:o + 4].view(torch.int32).item()) > 0
+    assert np.array_equal(out[0], out[1])
