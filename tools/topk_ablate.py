@@ -55,7 +55,7 @@ for dbg in (1, 4):
     tot = sv[6]
     o = wsk.numel() - 4 - 4 * nr  # workspace tail: ovf list, its count, then u32 seeds[q]
     n_ovf = int(wsk[o:o + 4].view(torch.int32).item())
-    print("dbg=%d: overflowed queries (f32 recompute) %d" % (dbg, n_ovf))
+    print("dbg=%d: overflowed queries (exact-mode relaunch) %d" % (dbg, n_ovf))
     print("dbg=%d: replays/wave %.0f firing tiles/wave %.0f appends/q %.0f compactions/q %.2f | shares: barrier %.3f, "
           "streaming %.3f, replays %.3f, final %.3f, other %.3f" %
           (dbg, sv[0] / waves, sv[1] / waves, sv[2] / nr, sv[3] / nr, sv[7] / tot, sv[9] / tot, sv[4] / tot,
