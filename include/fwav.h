@@ -74,7 +74,8 @@ int fwav_prune(const float* ranges, int64_t n, int64_t q_offset, int range_size,
 
 /* ------------------------------------------------------------------- similarity top-K
  * Replaces range_candidates_from_embedding_emb + pad_candidates (fractal.py:535-552, 617-622): for each
- * local query listed in active[0 .. *n_active) (at most max_q), the K domains with the largest f32 score
+ * local query listed in active[0 .. *n_active) (at most max_q entries; max_q bounds their number, not their
+ * values — a listed i only needs its cand row), the K domains with the largest f32 score
  * fma_k(emb[d][k]·emb[q_offset+i][k]) in (score desc, index asc) order, −1-padded when n_domains < K,
  * into cand[i·K .. i·K+K).  K ≤ 64: emb16 != NULL selects the fp16 MFMA pre-filter + exact f32 rescoring
  * kernel, emb16 == NULL the all-f32 MFMA kernel; both return identical candidates.  K > 64 (the module-global
