@@ -320,12 +320,14 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 // pair starts on a different chunk.  Neutral in same-box A/B (21.73 / 21.76 / 22.00 ms for 0 / 1 / 2); a static
 // s_setprio for the second half was slower (+3 %).
 // Exact mode (overflow relaunch) compacts every FWAV_TOPK_EXGROW appends, so its K-th exact key — the store filter —
-// and band limit rise sooner (cfg3: 32 / 64 / 96 / 128 / full buffer 859 / 861 / 870 / 887 / 898 ms)
+// and band limit rise sooner (cfg3 at δ = 2.5e-3: 32 / 64 / 96 / 128 / full buffer 859 / 861 / 870 / 887 / 898 ms;
+// at δ = 2.0e-3: 16 / 24 / 32 / 64 / 128 → 690 / 702 / 695–704 / 711–725 / 727 ms)
+#ifndef FWAV_TOPK_EXGROW
+#define FWAV_TOPK_EXGROW 32
+#endif
+// Exact-mode occupancy (waves per SIMD): 2 avoids its register spills but halves the workgroups per CU (856 vs 785 ms)
 #ifndef FWAV_TOPK_EXWPE
 #define FWAV_TOPK_EXWPE 4
-#endif
-#ifndef FWAV_TOPK_EXGROW
-#define FWAV_TOPK_EXGROW 64
 #endif
 #ifndef FWAV_TOPK_STAGGER
 #define FWAV_TOPK_STAGGER 0
