@@ -846,8 +846,11 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
 // the stream's own MFMA, recomputed per radix step (a greedy bitwise select over the non-negative keys, ballots
 // free: each query's two lanes combine their counts by one shuffle).  Returns −∞ when fewer than K window scores
 // are ≥ 0.
-constexpr int kSeedTiles = 6;
-constexpr int kSeedHalf = 64;
+#ifndef FWAV_TOPK_SEEDHALF
+#define FWAV_TOPK_SEEDHALF 64
+#endif
+constexpr int kSeedHalf = FWAV_TOPK_SEEDHALF;
+constexpr int kSeedTiles = (2 * kSeedHalf + 62) / 32 + 1;  // the wave's 32 windows from a tile-aligned base
 __device__ __forceinline__ float seed_limit(const _Float16* __restrict__ emb16, int64_t nd, half8 b, int64_t qrow,
                                             int64_t wbase, int K) {
   const int lane = threadIdx.x & 63;
