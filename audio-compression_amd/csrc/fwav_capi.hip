@@ -18,7 +18,7 @@ extern "C" {
 
 const char* fwav_last_error(void) { return fwav::g_err; }
 
-int fwav_abi_version(void) { return 1; }
+int fwav_abi_version(void) { return 2; }
 
 // Block until all work queued on `stream` is done; reports asynchronous kernel faults.
 int fwav_stream_sync(void* stream) {

@@ -8,58 +8,294 @@
 //                        : (valid ? s_opt : s_st); clip ±s_clip; next = s_used·T + o (bincount → +0.0 + x);
 //                        Δ = ‖next − rec‖ / (‖rec‖ or 1); stop when Δ < eps.
 //
-// T, mean(T), ‖T − mean T‖² and `valid` do not change across iterations: k_decode_prepare computes them
-// once.  Each iteration is one k_decode_iter launch (thread per range, f64 block partials of ‖rec‖² and
-// ‖next − rec‖²) and one single-block k_decode_check that sums the partials in a fixed order, records Δ and
-// raises a device flag; every later launch sees the flag and exits, so all `iterations` launches are
-// queued with no host synchronisation.  Δ is f64 here (BLAS sdot in the reference): only the early-exit
-// decision can differ, and only when Δ lies within rounding of eps.
-// Bytes per range per iteration: 4·rs (rec) + 4·rs (next) + 4·rs (T) + 16 (mean, den, s, o) + 1 (valid).
+// Iteration-resident design (range_size ≤ 32).  Within one iteration the ranges are independent, and a range's
+// next reconstruction depends only on its own previous one: the loop couples ranges through Δ alone.  So a
+// thread keeps its ranges' T (gathered once from the pool), T − mean T and the reconstruction in registers and
+// runs up to kDecIters iterations without touching HBM, adding its ‖rec‖² and ‖next − rec‖² contributions to
+// per-iteration f64 partials.  Per chunk of kDecIters iterations:
+//   k_decode_run     (grid: one block per kDecSpan ranges) → rec after the chunk + block partials[t][block]
+//   k_decode_sum     (grid: one block per iteration)       → Σ over blocks, fixed order
+//   k_decode_stop    (one wave)                            → Δ_t, first t with Δ_t < eps → state
+// and once at the end
+//   k_decode_run<finish>: if the loop stopped inside a chunk, recompute that chunk from its start state up to
+//                         the stopping iteration (same arithmetic, so the same values) into the result buffer.
+// HBM traffic is therefore ≈ (4·rs gathered + 13) B read + 4·rs B written per range per chunk, instead of
+// (12·rs + 17) B per range per iteration; the loop is bound by VALU issue.
+//
+// Δ is f64 here (BLAS sdot in the reference): only the early-exit decision can differ, and only when Δ lies
+// within rounding of eps.  The f64 sum has one canonical order — range → thread (sequential) → wave (xor tree)
+// → block (kDecSpan ranges, fixed) → sum over blocks (fixed) — so a range-sharded decode (fwav.dist) whose shard
+// bounds are multiples of kDecSpan adds exactly the same partials and reproduces Δ bit-for-bit at any world size:
+// the ranks all-reduce the block partials (one non-zero contributor per entry, so the reduction is exact).
+//
+// range_size > 32 uses the per-iteration streaming kernels at the end of this file (single device only).
 #include "fwav_common.h"
 #include "../../include/fwav.h"
 
 namespace fwav {
 
-constexpr int kDecThreads = 256;
+constexpr int kDecSpan = 4096;     // ranges per run block: the unit of the canonical Δ reduction
+constexpr int kDecIters = 64;      // iterations per run launch
+constexpr int kDecThreads = 256;   // run / sum block size (4 waves)
+constexpr int kDecWaves = kDecThreads / kWave;
 
-template <int RS>
+// numpy pairwise_sum (fwav_common.h pw_sum) of x[0..n) for a register array of RSMAX ≥ n floats: n ≤ 32 < 128,
+// so one leaf.  NFIX > 0 fixes n at compile time; otherwise n is runtime-uniform and every index stays constant
+// (guarded), so the array never leaves registers.
+template <int RSMAX, int NFIX, class F>
+__device__ __forceinline__ float pw_reg(const F& f, int n_rt) {
+  const int n = NFIX > 0 ? NFIX : n_rt;
+  if constexpr (NFIX > 0) {
+    return pw_sum_n<NFIX>(f);
+  } else {
+    float res;
+    if (n < 8) {
+      float r = 0.0f;
+#pragma unroll
+      for (int i = 0; i < (RSMAX < 8 ? RSMAX : 8); ++i)
+        if (i < n) r = r + f(i);
+      res = r;
+    } else {
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = f(j);
+      const int m = n - (n & 7);
+#pragma unroll
+      for (int i = 8; i < RSMAX; i += 8)
+        if (i < m) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = r[j] + f(i + j);
+        }
+      res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+      for (int i = 8; i < RSMAX; ++i)
+        if (i >= m && i < n) res = res + f(i);
+    }
+    return 0.0f + res;
+  }
+}
+
+struct DecArgs {
+  const int32_t* idx;
+  const float* s;
+  const float* o;
+  const uint8_t* sym;
+  const float* pool;
+  float* buf_a;
+  float* buf_b;
+  double* partials;   // [kDecIters][nblk_g][2]
+  int* state;         // done, iterations run, result buffer (0 = a, 1 = b), stop chunk
+  int64_t m;          // local ranges (this shard)
+  int64_t blk0;       // global block index of local range 0 (shard lo / kDecSpan)
+  int64_t nblk_g;     // blocks of the whole (unsharded) signal
+  int rs;
+  int iterations;
+  int chunk;
+  float s_clip;
+  float c_keep;
+  float c_opt;
+  int use_damping;
+};
+
+// Chunk buffers: X_0 = zeros (virtual), X_k = buf_b for odd k, buf_a for even k ≥ 2.  Chunk k reads X_k and
+// writes X_{k+1}; the result is X_{stop chunk + 1}.
+__device__ __forceinline__ float* dec_buf(const DecArgs& a, int k) { return (k & 1) ? a.buf_b : a.buf_a; }
+
+template <int RSMAX, int NFIX, int G, bool FINISH>
+__global__ __launch_bounds__(kDecThreads) void k_decode_run(DecArgs a) {
+  __shared__ double acc[kDecIters][kDecWaves][2];
+  int k, t0, nit;
+  if constexpr (FINISH) {
+    if (a.state[0] == 0) return;  // ran every iteration: the last chunk's output is the result
+    k = a.state[3];
+    t0 = k * kDecIters;
+    nit = a.state[1] - t0;
+    if (nit == min(kDecIters, a.iterations - t0)) return;  // stopped at the chunk's last iteration: already there
+  } else {
+    if (a.state[0] != 0) return;
+    k = a.chunk;
+    t0 = k * kDecIters;
+    nit = min(kDecIters, a.iterations - t0);
+  }
+  const float* rin = k == 0 ? nullptr : dec_buf(a, k);
+  float* rout = dec_buf(a, k + 1);
+  const int rs = NFIX > 0 ? NFIX : a.rs;
+  if constexpr (!FINISH) {
+    for (int j = threadIdx.x; j < kDecIters * kDecWaves * 2; j += kDecThreads) (&acc[0][0][0])[j] = 0.0;
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kDecSpan;
+  for (int g = 0; g < kDecSpan / (kDecThreads * G); ++g) {
+    const int64_t r0 = base + ((int64_t)g * kDecThreads + threadIdx.x) * G;
+    float T[G][RSMAX], tc[G][RSMAX], rec[G][RSMAX];
+    float den[G], sst[G], ost[G];
+    bool valid[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int64_t r = r0 + u;
+      const bool live = r < a.m;
+      const int32_t i0 = live ? a.idx[r] : -1;
+      const bool inval = i0 < 0;
+      const bool sy = inval ? false : (a.sym[r] != 0);
+      const float* D = a.pool + (int64_t)(inval ? 0 : i0) * rs;
+#pragma unroll
+      for (int i = 0; i < RSMAX; ++i) {
+        float v = 0.0f;
+        if (i < rs && !inval) v = sy ? D[rs - 1 - i] : D[i];
+        T[u][i] = v;
+      }
+      const float md = pw_reg<RSMAX, NFIX>([&](int i) { return T[u][i]; }, rs) / (float)rs;
+#pragma unroll
+      for (int i = 0; i < RSMAX; ++i) tc[u][i] = T[u][i] - md;
+      den[u] = pw_reg<RSMAX, NFIX>([&](int i) { return tc[u][i] * tc[u][i]; }, rs);
+      valid[u] = den[u] > 1e-12f;
+      sst[u] = inval ? 0.0f : a.s[r];
+      ost[u] = inval ? 0.0f : a.o[r];
+#pragma unroll
+      for (int i = 0; i < RSMAX; ++i) rec[u][i] = (rin != nullptr && live && i < rs) ? rin[r * rs + i] : 0.0f;
+    }
+    for (int t = 0; t < nit; ++t) {
+      double rn = 0.0, dn = 0.0;
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const float mr = pw_reg<RSMAX, NFIX>([&](int i) { return rec[u][i]; }, rs) / (float)rs;
+        const float num = pw_reg<RSMAX, NFIX>([&](int i) { return (rec[u][i] - mr) * tc[u][i]; }, rs);
+        const float s_opt = valid[u] ? num / den[u] : 0.0f;
+        float su = a.use_damping ? a.c_keep * sst[u] + a.c_opt * s_opt : (valid[u] ? s_opt : sst[u]);
+        su = clip_sym(su, a.s_clip);
+#pragma unroll
+        for (int i = 0; i < RSMAX; ++i) {
+          if (i < rs) {
+            const float x = 0.0f + (su * T[u][i] + ost[u]);
+            const float df = x - rec[u][i];                 // recon_next − recon in f32 (fractal.py:1460)
+            rn = fma((double)rec[u][i], (double)rec[u][i], rn);  // exact product: == rn + x·x
+            dn = fma((double)df, (double)df, dn);
+            rec[u][i] = x;
+          }
+        }
+      }
+      if constexpr (!FINISH) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          rn += __shfl_xor(rn, off);
+          dn += __shfl_xor(dn, off);
+        }
+        if (lane == 0) {
+          acc[t][wave][0] += rn;
+          acc[t][wave][1] += dn;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int64_t r = r0 + u;
+      if (r < a.m) {
+#pragma unroll
+        for (int i = 0; i < RSMAX; ++i)
+          if (i < rs) rout[r * rs + i] = rec[u][i];
+      }
+    }
+  }
+  if constexpr (!FINISH) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < nit; t += kDecThreads) {
+      double* p = a.partials + ((int64_t)t * a.nblk_g + a.blk0 + blockIdx.x) * 2;
+      p[0] = (acc[t][0][0] + acc[t][1][0]) + (acc[t][2][0] + acc[t][3][0]);
+      p[1] = (acc[t][0][1] + acc[t][1][1]) + (acc[t][2][1] + acc[t][3][1]);
+    }
+  }
+}
+
+// One block per iteration t of the chunk: Σ over the nblk_g block partials in a fixed order → sums[t].
+__global__ __launch_bounds__(kDecThreads) void k_decode_sum(const double* __restrict__ partials, int64_t nblk_g,
+                                                            double* __restrict__ sums, const int* __restrict__ state,
+                                                            int chunk, int iterations) {
+  __shared__ double red[kDecWaves][2];
+  if (state[0] != 0) return;
+  const int t = blockIdx.x;
+  if (t >= min(kDecIters, iterations - chunk * kDecIters)) return;
+  const double* p = partials + (int64_t)t * nblk_g * 2;
+  double a = 0.0, b = 0.0;
+  for (int64_t j = threadIdx.x; j < nblk_g; j += kDecThreads) {
+    a += p[2 * j];
+    b += p[2 * j + 1];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6][0] = a;
+    red[threadIdx.x >> 6][1] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sums[2 * t] = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+    sums[2 * t + 1] = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+  }
+}
+
+// Δ_t for the chunk's iterations in order; the first Δ_t < eps stops the loop.
+__global__ void k_decode_stop(const double* __restrict__ sums, int chunk, int iterations, double eps,
+                              int* __restrict__ state, double* __restrict__ deltas) {
+  if (threadIdx.x != 0 || state[0] != 0) return;
+  const int t0 = chunk * kDecIters;
+  const int nit = min(kDecIters, iterations - t0);
+  for (int t = 0; t < nit; ++t) {
+    const double nrm = sqrt(sums[2 * t]);
+    const double delta = sqrt(sums[2 * t + 1]) / (nrm > 0.0 ? nrm : 1.0);
+    deltas[t0 + t] = delta;
+    if (delta < eps) {
+      state[0] = 1;
+      state[1] = t0 + t + 1;
+      state[2] = ((chunk + 1) & 1) ? 1 : 0;
+      state[3] = chunk;
+      return;
+    }
+  }
+  state[1] = t0 + nit;
+  state[2] = ((chunk + 1) & 1) ? 1 : 0;
+  state[3] = chunk;
+}
+
+// ------------------------------------------------------------------ range_size > 32: streaming kernels
+// One launch pair per iteration: k_decode_prepare gathers T once; k_decode_iter (thread per range, f64 block
+// partials) + k_decode_check (fixed-order sum, Δ, flag).  Later launches exit on the flag.
+constexpr int kStreamThreads = 256;
+
 __global__ void k_decode_prepare(const int32_t* __restrict__ idx, const float* __restrict__ s_in,
                                  const float* __restrict__ o_in, const uint8_t* __restrict__ sym_in, int64_t nr,
-                                 int rs_rt, const float* __restrict__ pool, float* __restrict__ T,
-                                 float* __restrict__ md, float* __restrict__ den, float* __restrict__ sst,
-                                 float* __restrict__ ost, uint8_t* __restrict__ valid) {
+                                 int rs, const float* __restrict__ pool, float* __restrict__ T, float* __restrict__ md,
+                                 float* __restrict__ den, float* __restrict__ sst, float* __restrict__ ost) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nr) return;
-  const int rs = RS > 0 ? RS : rs_rt;
   const int32_t i0 = idx[r];
   const bool inval = i0 < 0;
   const bool sym = inval ? false : (sym_in[r] != 0);
   const float* D = pool + (int64_t)(inval ? 0 : i0) * rs;
   float* Tr = T + r * rs;
   for (int i = 0; i < rs; ++i) Tr[i] = inval ? 0.0f : (sym ? D[rs - 1 - i] : D[i]);
-  auto ft = [&](int i) { return Tr[i]; };
-  const float m = pw_sum(ft, rs) / (float)rs;
-  auto fd = [&](int i) {
-    const float t = Tr[i] - m;
-    return t * t;
-  };
-  const float dd = pw_sum(fd, rs);
+  const float m = pw_sum([&](int i) { return Tr[i]; }, rs) / (float)rs;
+  den[r] = pw_sum(
+      [&](int i) {
+        const float t = Tr[i] - m;
+        return t * t;
+      },
+      rs);
   md[r] = m;
-  den[r] = dd;
-  valid[r] = dd > 1e-12f;
   sst[r] = inval ? 0.0f : s_in[r];
   ost[r] = inval ? 0.0f : o_in[r];
 }
 
-template <int RS>
-__global__ __launch_bounds__(kDecThreads) void k_decode_iter(
+__global__ __launch_bounds__(kStreamThreads) void k_decode_iter(
     const float* __restrict__ T, const float* __restrict__ md, const float* __restrict__ den,
-    const float* __restrict__ sst, const float* __restrict__ ost, const uint8_t* __restrict__ valid, int64_t nr,
-    int rs_rt, float s_clip, float c_keep, float c_opt, int use_damping, const float* __restrict__ rec,
-    float* __restrict__ nxt, double* __restrict__ partial, const int* __restrict__ done) {
-  __shared__ double red[2][kDecThreads / kWave];
-  if (*done) return;
-  const int rs = RS > 0 ? RS : rs_rt;
+    const float* __restrict__ sst, const float* __restrict__ ost, int64_t nr, int rs, float s_clip, float c_keep,
+    float c_opt, int use_damping, const float* __restrict__ rec, float* __restrict__ nxt,
+    double* __restrict__ partial, const int* __restrict__ state) {
+  __shared__ double red[2][kStreamThreads / kWave];
+  if (state[0]) return;
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double rn = 0.0, dn = 0.0;
   if (r < nr) {
@@ -67,11 +303,9 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_iter(
     const float* Rr = rec + r * rs;
     float* Nr = nxt + r * rs;
     const float m = md[r];
-    auto fr = [&](int i) { return Rr[i]; };
-    const float mr = pw_sum(fr, rs) / (float)rs;
-    auto fn = [&](int i) { return (Rr[i] - mr) * (Tr[i] - m); };
-    const float num = pw_sum(fn, rs);
-    const bool v = valid[r] != 0;
+    const float mr = pw_sum([&](int i) { return Rr[i]; }, rs) / (float)rs;
+    const float num = pw_sum([&](int i) { return (Rr[i] - mr) * (Tr[i] - m); }, rs);
+    const bool v = den[r] > 1e-12f;
     const float s_opt = v ? num / den[r] : 0.0f;
     float su = use_damping ? c_keep * sst[r] + c_opt * s_opt : (v ? s_opt : sst[r]);
     su = clip_sym(su, s_clip);
@@ -81,8 +315,8 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_iter(
       const float old = Rr[i];
       const float df = x - old;
       Nr[i] = x;
-      rn += (double)old * (double)old;
-      dn += (double)df * (double)df;
+      rn = fma((double)old, (double)old, rn);
+      dn = fma((double)df, (double)df, dn);
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -95,17 +329,16 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_iter(
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double a = 0.0, b = 0.0;
-    for (int j = 0; j < kDecThreads / kWave; ++j) {
-      a += red[0][j];
-      b += red[1][j];
+    double x = 0.0, y = 0.0;
+    for (int j = 0; j < kStreamThreads / kWave; ++j) {
+      x += red[0][j];
+      y += red[1][j];
     }
-    partial[2 * blockIdx.x] = a;
-    partial[2 * blockIdx.x + 1] = b;
+    partial[2 * blockIdx.x] = x;
+    partial[2 * blockIdx.x + 1] = y;
   }
 }
 
-// One block: Δ for iteration `it`, convergence flag, iteration counter.  state: int done, int iters_run.
 __global__ void k_decode_check(const double* __restrict__ partial, int nblocks, int it, double eps,
                                int* __restrict__ state, double* __restrict__ deltas) {
   __shared__ double red[2][1024 / kWave];
@@ -134,8 +367,55 @@ __global__ void k_decode_check(const double* __restrict__ partial, int nblocks, 
     const double delta = sqrt(dn) / (nrm > 0.0 ? nrm : 1.0);
     deltas[it] = delta;
     state[1] = it + 1;
+    state[2] = ((it + 1) & 1) ? 1 : 0;  // iteration it wrote recon_b when it is even
     if (delta < eps) state[0] = 1;
   }
+}
+
+constexpr int kMaxResidentRs = 32;
+
+int64_t dec_blocks(int64_t nr) { return cdiv(nr > 0 ? nr : 1, kDecSpan); }
+
+// Launch the run kernel for the bucket of rs (G ranges per thread keeps ≈ 3·G·rs floats in registers).
+template <bool FINISH>
+void launch_run(const DecArgs& a, int64_t nblk_local, hipStream_t st) {
+  const dim3 grid((unsigned)nblk_local), block(kDecThreads);
+  switch (a.rs) {
+    case 4: k_decode_run<4, 4, 4, FINISH><<<grid, block, 0, st>>>(a); break;
+    case 8: k_decode_run<8, 8, 4, FINISH><<<grid, block, 0, st>>>(a); break;
+    case 16: k_decode_run<16, 16, 2, FINISH><<<grid, block, 0, st>>>(a); break;
+    case 32: k_decode_run<32, 32, 1, FINISH><<<grid, block, 0, st>>>(a); break;
+    default:
+      if (a.rs < 8) k_decode_run<8, 0, 4, FINISH><<<grid, block, 0, st>>>(a);
+      else if (a.rs < 16) k_decode_run<16, 0, 2, FINISH><<<grid, block, 0, st>>>(a);
+      else k_decode_run<32, 0, 1, FINISH><<<grid, block, 0, st>>>(a);
+  }
+}
+
+DecArgs make_args(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t m, int64_t lo,
+                  int64_t nr_global, int rs, const float* pool, int iterations, int chunk, float s_clip,
+                  double s_damping, float* a, float* b, double* partials, int* state) {
+  DecArgs d;
+  d.idx = idx;
+  d.s = s;
+  d.o = o;
+  d.sym = sym;
+  d.pool = pool;
+  d.buf_a = a;
+  d.buf_b = b;
+  d.partials = partials;
+  d.state = state;
+  d.m = m;
+  d.blk0 = lo / kDecSpan;
+  d.nblk_g = dec_blocks(nr_global);
+  d.rs = rs;
+  d.iterations = iterations;
+  d.chunk = chunk;
+  d.s_clip = fabsf(s_clip);
+  d.c_keep = (float)(1.0 - s_damping);  // Python float (1.0 - d) meets an f32 array (NEP 50)
+  d.c_opt = (float)s_damping;
+  d.use_damping = s_damping > 0.0;
+  return d;
 }
 
 }  // namespace fwav
@@ -144,27 +424,118 @@ using namespace fwav;
 
 extern "C" {
 
-size_t fwav_decode_workspace_size(int64_t nr, int rs, int iterations) {
-  const int64_t nb = cdiv(nr > 0 ? nr : 1, kDecThreads);
-  return (size_t)(nr * rs * 4 * 3 + nr * 4 * 4 + nr + 64 + nb * 2 * 8 + 64);
+int fwav_decode_span(void) { return kDecSpan; }
+int fwav_decode_chunk_iterations(void) { return kDecIters; }
+
+size_t fwav_decode_partials_count(int64_t nr_global) {
+  return (size_t)(kDecIters * dec_blocks(nr_global) * 2 + kDecIters * 2);
 }
 
-// Full decode loop.  recon_a / recon_b: f32[nr*rs] ping-pong buffers (recon_a is zeroed here); after the
-// call, iteration count state[1] = t selects the result: t odd → recon_b, t even → recon_a.
-// deltas: f64[iterations].  state: int[2] on device.
+size_t fwav_decode_workspace_size(int64_t nr, int rs, int iterations) {
+  (void)iterations;
+  if (rs <= kMaxResidentRs) return fwav_decode_partials_count(nr) * sizeof(double) + 64;
+  const int64_t nb = cdiv(nr > 0 ? nr : 1, kStreamThreads);
+  return (size_t)(nr * rs * 4 + nr * 4 * 4 + 64 + nb * 2 * 8 + 64);
+}
+
+static int check_common(const void* idx, const void* s, const void* o, const void* sym, const void* pool,
+                        const void* a, const void* b, const void* state, int64_t nr, int rs, int iterations,
+                        const char* who) {
+  FWAV_CHECK_ARG(idx && s && o && sym && pool && a && b && state, FWAV_ERR_ARG, "%s: null pointer", who);
+  FWAV_CHECK_ARG(nr >= 0 && rs >= 1 && rs <= kMaxPairwise && iterations >= 0, FWAV_ERR_SHAPE, "%s: shape", who);
+  return FWAV_OK;
+}
+
+// Sharded building blocks (the single-device fwav_decode below is exactly this sequence with lo = 0, m = nr).
+int fwav_decode_run(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t m,
+                    int64_t lo, int64_t nr_global, int rs, const float* pool, int64_t nd, int iterations, int chunk,
+                    float s_clip, double s_damping, float* recon_a, float* recon_b, double* partials, int* state,
+                    void* stream) {
+  int rc = check_common(idx, s_in, o_in, sym, pool, recon_a, recon_b, state, m, rs, iterations, "fwav_decode_run");
+  if (rc) return rc;
+  FWAV_CHECK_ARG(partials, FWAV_ERR_ARG, "fwav_decode_run: null partials");
+  FWAV_CHECK_ARG(rs <= kMaxResidentRs, FWAV_ERR_SHAPE, "fwav_decode_run: range_size %d > %d", rs, kMaxResidentRs);
+  FWAV_CHECK_ARG(lo >= 0 && lo % kDecSpan == 0 && lo + m <= nr_global && (lo + m == nr_global || m % kDecSpan == 0),
+                 FWAV_ERR_SHAPE, "fwav_decode_run: shard [%lld, %lld) of %lld not aligned to %d ranges",
+                 (long long)lo, (long long)(lo + m), (long long)nr_global, kDecSpan);
+  FWAV_CHECK_ARG(chunk >= 0 && (int64_t)chunk * kDecIters < iterations, FWAV_ERR_ARG, "fwav_decode_run: chunk");
+  (void)nd;
+  hipStream_t st = (hipStream_t)stream;
+  if (chunk == 0) (void)hipMemsetAsync(state, 0, 4 * sizeof(int), st);
+  if (m != nr_global)  // other ranks' blocks must add exactly zero in the all-reduce
+    (void)hipMemsetAsync(partials, 0, (size_t)kDecIters * dec_blocks(nr_global) * 2 * sizeof(double), st);
+  if (m > 0) {
+    DecArgs d = make_args(idx, s_in, o_in, sym, m, lo, nr_global, rs, pool, iterations, chunk, s_clip, s_damping,
+                          recon_a, recon_b, partials, state);
+    launch_run<false>(d, dec_blocks(m), st);
+  }
+  FWAV_LAUNCH_CHECK("fwav_decode_run");
+  return FWAV_OK;
+}
+
+int fwav_decode_reduce(const double* partials, int64_t nr_global, int iterations, int chunk, double eps,
+                       double* deltas, int* state, void* stream) {
+  FWAV_CHECK_ARG(partials && deltas && state, FWAV_ERR_ARG, "fwav_decode_reduce: null pointer");
+  FWAV_CHECK_ARG(chunk >= 0 && (int64_t)chunk * kDecIters < iterations, FWAV_ERR_ARG, "fwav_decode_reduce: chunk");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nb = dec_blocks(nr_global);
+  double* sums = (double*)partials + (int64_t)kDecIters * nb * 2;
+  k_decode_sum<<<kDecIters, kDecThreads, 0, st>>>(partials, nb, sums, state, chunk, iterations);
+  k_decode_stop<<<1, kWave, 0, st>>>(sums, chunk, iterations, eps, state, deltas);
+  FWAV_LAUNCH_CHECK("fwav_decode_reduce");
+  return FWAV_OK;
+}
+
+int fwav_decode_finish(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t m,
+                       int64_t lo, int64_t nr_global, int rs, const float* pool, int64_t nd, int iterations,
+                       float s_clip, double s_damping, float* recon_a, float* recon_b, int* state, void* stream) {
+  int rc = check_common(idx, s_in, o_in, sym, pool, recon_a, recon_b, state, m, rs, iterations, "fwav_decode_finish");
+  if (rc) return rc;
+  FWAV_CHECK_ARG(rs <= kMaxResidentRs, FWAV_ERR_SHAPE, "fwav_decode_finish: range_size %d > %d", rs, kMaxResidentRs);
+  (void)nd;
+  hipStream_t st = (hipStream_t)stream;
+  if (m > 0 && iterations > 0) {
+    DecArgs d = make_args(idx, s_in, o_in, sym, m, lo, nr_global, rs, pool, iterations, 0, s_clip, s_damping,
+                          recon_a, recon_b, nullptr, state);
+    launch_run<true>(d, dec_blocks(m), st);
+  }
+  FWAV_LAUNCH_CHECK("fwav_decode_finish");
+  return FWAV_OK;
+}
+
+// Full decode loop on one device.  recon_a / recon_b: f32[nr*rs] buffers; after the call state[1] = iterations
+// run and state[2] selects the result (0 → recon_a, 1 → recon_b).  deltas: f64[iterations].  state: int[4].
 int fwav_decode(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t nr, int rs,
                 const float* pool, int64_t nd, int iterations, double eps, float s_clip, double s_damping,
                 float* recon_a, float* recon_b, double* deltas, int* state, void* workspace, size_t ws_bytes,
                 void* stream) {
-  FWAV_CHECK_ARG(idx && s_in && o_in && sym && pool && recon_a && recon_b && state, FWAV_ERR_ARG,
-                 "fwav_decode: null pointer");
-  FWAV_CHECK_ARG(nr >= 0 && rs >= 1 && rs <= kMaxPairwise && iterations >= 0, FWAV_ERR_SHAPE, "fwav_decode: shape");
+  int rc = check_common(idx, s_in, o_in, sym, pool, recon_a, recon_b, state, nr, rs, iterations, "fwav_decode");
+  if (rc) return rc;
   FWAV_CHECK_ARG(ws_bytes >= fwav_decode_workspace_size(nr, rs, iterations) && workspace, FWAV_ERR_WORKSPACE,
                  "fwav_decode: workspace too small");
   FWAV_CHECK_ARG(iterations == 0 || deltas, FWAV_ERR_ARG, "fwav_decode: deltas required");
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(state, 0, 2 * sizeof(int), st);
+  (void)hipMemsetAsync(state, 0, 4 * sizeof(int), st);
   if (nr == 0) return FWAV_OK;
+  if (iterations == 0) {  // the reference returns its zero-initialised buffer
+    (void)hipMemsetAsync(recon_a, 0, (size_t)nr * rs * sizeof(float), st);
+    FWAV_LAUNCH_CHECK("fwav_decode");
+    return FWAV_OK;
+  }
+  double* partials = (double*)(((uintptr_t)workspace + 63) & ~(uintptr_t)63);
+  if (rs <= kMaxResidentRs) {
+    const int nchunks = (int)cdiv(iterations, kDecIters);
+    for (int c = 0; c < nchunks; ++c) {
+      rc = fwav_decode_run(idx, s_in, o_in, sym, nr, 0, nr, rs, pool, nd, iterations, c, s_clip, s_damping, recon_a,
+                           recon_b, partials, state, stream);
+      if (rc) return rc;
+      rc = fwav_decode_reduce(partials, nr, iterations, c, eps, deltas, state, stream);
+      if (rc) return rc;
+    }
+    return fwav_decode_finish(idx, s_in, o_in, sym, nr, 0, nr, rs, pool, nd, iterations, s_clip, s_damping, recon_a,
+                              recon_b, state, stream);
+  }
+  // range_size > 32: per-iteration streaming
   (void)hipMemsetAsync(recon_a, 0, (size_t)nr * rs * sizeof(float), st);
   char* w = (char*)workspace;
   float* T = (float*)w;
@@ -172,32 +543,20 @@ int fwav_decode(const int32_t* idx, const float* s_in, const float* o_in, const 
   float* den = md + nr;
   float* sst = den + nr;
   float* ost = sst + nr;
-  uint8_t* valid = (uint8_t*)(ost + nr);
-  double* partial = (double*)(((uintptr_t)(valid + nr) + 63) & ~(uintptr_t)63);
-  const int64_t nb = cdiv(nr, kDecThreads);
-  const float c_keep = (float)(1.0 - s_damping);  // Python float (1.0 - d) meets an f32 array (NEP 50)
+  double* partial = (double*)(((uintptr_t)(ost + nr) + 63) & ~(uintptr_t)63);
+  const int64_t nb = cdiv(nr, kStreamThreads);
+  const float c_keep = (float)(1.0 - s_damping);
   const float c_opt = (float)s_damping;
   const int use_d = s_damping > 0.0;
   const float clipc = fabsf(s_clip);
-#define FWAV_DEC(RSV)                                                                                             \
-  do {                                                                                                            \
-    k_decode_prepare<RSV><<<nb, kDecThreads, 0, st>>>(idx, s_in, o_in, sym, nr, rs, pool, T, md, den, sst, ost,  \
-                                                      valid);                                                     \
-    for (int it = 0; it < iterations; ++it) {                                                                     \
-      const float* rec = (it & 1) ? recon_b : recon_a;                                                            \
-      float* nx = (it & 1) ? recon_a : recon_b;                                                                   \
-      k_decode_iter<RSV><<<nb, kDecThreads, 0, st>>>(T, md, den, sst, ost, valid, nr, rs, clipc, c_keep, c_opt,  \
-                                                     use_d, rec, nx, partial, state);                             \
-      k_decode_check<<<1, 1024, 0, st>>>(partial, (int)nb, it, eps, state, deltas);                               \
-    }                                                                                                             \
-  } while (0)
-  switch (rs) {
-    case 4: FWAV_DEC(4); break;
-    case 8: FWAV_DEC(8); break;
-    case 16: FWAV_DEC(16); break;
-    default: FWAV_DEC(0); break;
+  k_decode_prepare<<<nb, kStreamThreads, 0, st>>>(idx, s_in, o_in, sym, nr, rs, pool, T, md, den, sst, ost);
+  for (int it = 0; it < iterations; ++it) {
+    const float* rec = (it & 1) ? recon_b : recon_a;
+    float* nx = (it & 1) ? recon_a : recon_b;
+    k_decode_iter<<<nb, kStreamThreads, 0, st>>>(T, md, den, sst, ost, nr, rs, clipc, c_keep, c_opt, use_d, rec, nx,
+                                                 partial, state);
+    k_decode_check<<<1, 1024, 0, st>>>(partial, (int)nb, it, eps, state, deltas);
   }
-#undef FWAV_DEC
   FWAV_LAUNCH_CHECK("fwav_decode");
   return FWAV_OK;
 }

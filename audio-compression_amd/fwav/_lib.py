@@ -38,6 +38,12 @@ SIGNATURES = {
     "fwav_affine": (I32, [P, I64, I32, P, I32, P, I64, F32, P, P, P, P, P, P]),
     "fwav_decode_workspace_size": (SZ, [I64, I32, I32]),
     "fwav_decode": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, SZ, P]),
+    "fwav_decode_span": (I32, []),
+    "fwav_decode_chunk_iterations": (I32, []),
+    "fwav_decode_partials_count": (SZ, [I64]),
+    "fwav_decode_run": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, I32, F32, F64, P, P, P, P, P]),
+    "fwav_decode_reduce": (I32, [P, I64, I32, I32, F64, P, P, P]),
+    "fwav_decode_finish": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, F32, F64, P, P, P, P]),
 }
 
 

@@ -1,20 +1,29 @@
-"""Multi-GPU compress: ranges of ONE signal sharded across ranks (one process per GPU, torch.distributed).
+"""Multi-GPU compress and decompress of ONE signal, ranges sharded across ranks (one process per GPU,
+torch.distributed; backend "nccl" is RCCL over xGMI on ROCm).
 
-Exchange pattern:
-  1. rank 0 holds the signal; ONE broadcast of the raw signal (f32, 4 B/sample: 691 MB at cfg4) over
-     RCCL/xGMI.  Broadcasting the signal instead of the domain pool (2.76 GB at cfg4) is cheaper and
-     sufficient: every rank rebuilds voiced mask, ranges, pool and embeddings bit-identically in a few ms,
-     whereas the pool alone would not give the ranges (they need the signal and the voiced-state scan over
-     the whole signal).
-  2. each rank searches + solves a contiguous block of ranges, blocks balanced by the number of ranges
-     that survive the energy prune (silent stretches cost nothing);
-  3. the SoA match arrays (17 B/range) are all-gathered into rank 0's result.
-No collective runs inside the search itself.  The per-rank compute is pluggable (``compute``) so the
-communication code is exercised on CPU with the gloo backend in tests; the product default is
-:func:`fwav.engine.compress_device` on the rank's GPU.
+Compress (reference split ``np.array_split`` of ranges over workers, fractal.py:1180-1182):
+  1. rank 0 holds the signal; ONE broadcast of the raw signal (f32, 4 B/sample: 691 MB at cfg4).  Broadcasting
+     the signal instead of the domain pool (2.76 GB at cfg4) moves 4× fewer bytes and is sufficient: every rank
+     rebuilds voiced mask, ranges, pool and embeddings bit-identically in a few ms (the ranges need the signal and
+     the voiced-state scan over the whole signal, so the pool alone would not do);
+  2. every rank computes the same contiguous range blocks, balanced by the ranges that survive the energy prune
+     (mean(r²) of the voiced-masked ranges the search will actually see; silent stretches cost nothing);
+  3. each rank searches + solves its block; the SoA match arrays (17 B/range) are gathered to rank 0, the only
+     rank that writes the .fwav.  No collective runs inside the search.
+
+Decompress (cfg5; fractal.py:1378-1473): rank 0 broadcasts the pool and scatters the match arrays; each rank runs
+the iteration-resident decode kernel on its ranges; per chunk of up to 64 iterations the ranks all-reduce the
+per-block Δ partials (a few hundred KB) and take the same early-exit decision; the reconstruction is gathered to
+rank 0.  Shard bounds are multiples of ``fwav_decode_span()`` ranges, so Δ, the iteration count and the output
+are bit-identical to the single-GPU decode at any world size (fwav_decode.hip header).
+
+Collectives run on device tensors with RCCL and on host tensors with gloo (CPU tests, and the one-GPU rehearsal
+where ranks share cuda:0).  The per-rank compute is pluggable (``compute`` / ``decoder``) so the communication
+code is exercised on CPU in tests; the product defaults are the HIP engine on the rank's GPU.
 """
 from __future__ import annotations
 
+import time
 from typing import Callable, Optional
 
 import numpy as np
@@ -24,6 +33,28 @@ import torch.distributed as dist
 from .engine import geometry
 
 FIELDS = ("idx", "s", "o", "sym", "err")
+
+
+# ------------------------------------------------------------------------------------------------ helpers
+def _coll_device(group, device: torch.device) -> torch.device:
+    """Where collective buffers live: the GPU for RCCL, the host for gloo."""
+    return device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+
+def _broadcast_(t: torch.Tensor, group, device: torch.device) -> torch.Tensor:
+    cd = _coll_device(group, device)
+    if t.device == cd:
+        dist.broadcast(t, src=0, group=group)
+        return t
+    buf = t.to(cd)
+    dist.broadcast(buf, src=0, group=group)
+    t.copy_(buf)
+    return t
+
+
+def _sync(device: torch.device) -> None:
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
 
 
 def balanced_bounds(weights: np.ndarray, world: int) -> list[tuple[int, int]]:
@@ -37,28 +68,49 @@ def balanced_bounds(weights: np.ndarray, world: int) -> list[tuple[int, int]]:
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
 
 
-def approx_active_weights(sig: torch.Tensor, range_size: int, energy_thresh: float) -> np.ndarray:
-    """Scheduling heuristic only (the exact prune runs inside each rank's compute): 1 for ranges whose raw
-    mean energy clears the prune threshold, else 0."""
-    n = sig.numel()
-    nr = -(-n // range_size)
-    x = torch.zeros(nr * range_size, dtype=torch.float32, device=sig.device)
-    x[:n] = sig
-    e = (x.view(nr, range_size).double() ** 2).mean(dim=1)
-    return (e >= 0.75 * energy_thresh).cpu().numpy().astype(np.float64)
+def prune_balanced_bounds(ranges: torch.Tensor, n_ranges: int, range_size: int, energy_thresh: float,
+                          world: int) -> list[tuple[int, int]]:
+    """Range blocks balanced by the energy prune of cpu_worker (fractal.py:601-603): a range whose voiced-masked
+    mean(r²) clears float32(0.75·thr) costs one full-table search (weight 1024), a pruned one almost nothing
+    (weight 1).  Integer weights and an integer cumsum, so every rank derives the same bounds from its own
+    (bit-identical) ranges with no collective.  Scheduling only: the exact prune runs inside each rank's search."""
+    x = ranges[:n_ranges * range_size].view(n_ranges, range_size)
+    thr = float(np.float32(energy_thresh * 0.75))
+    active = (x.double().square().mean(dim=1) >= thr).to(torch.int64)
+    cs = torch.cumsum(active * 1023 + 1, dim=0)
+    total = int(cs[-1].item()) if n_ranges else 0
+    targets = torch.tensor([total * r // world for r in range(1, world)], dtype=torch.int64, device=cs.device)
+    cuts = torch.searchsorted(cs, targets, right=True).cpu().tolist() if world > 1 else []
+    cuts = [0] + [min(int(c), n_ranges) for c in cuts] + [n_ranges]
+    cuts = np.maximum.accumulate(cuts)
+    return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
 
 
 def _pack(fields: dict, length: int, device) -> torch.Tensor:
     out = torch.zeros((5, length), dtype=torch.int32, device=device)
     m = len(fields["idx"])
-    out[0, :m] = fields["idx"].to(torch.int32)
-    out[1, :m] = fields["s"].view(torch.int32)
-    out[2, :m] = fields["o"].view(torch.int32)
-    out[3, :m] = fields["sym"].to(torch.int32)
-    out[4, :m] = fields["err"].view(torch.int32)
+    out[0, :m] = fields["idx"].to(device=device, dtype=torch.int32)
+    out[1, :m] = fields["s"].to(device).view(torch.int32)
+    out[2, :m] = fields["o"].to(device).view(torch.int32)
+    out[3, :m] = fields["sym"].to(device=device, dtype=torch.int32)
+    out[4, :m] = fields["err"].to(device).view(torch.int32)
     return out
 
 
+def _unpack(packed: torch.Tensor, blocks) -> dict:
+    parts = {f: [] for f in FIELDS}
+    for r, (a, b) in enumerate(blocks):
+        m = b - a
+        p = packed[r]
+        parts["idx"].append(p[0, :m])
+        parts["s"].append(p[1, :m].view(torch.float32))
+        parts["o"].append(p[2, :m].view(torch.float32))
+        parts["sym"].append(p[3, :m].to(torch.uint8))
+        parts["err"].append(p[4, :m].view(torch.float32))
+    return {f: torch.cat(v) for f, v in parts.items()}
+
+
+# ------------------------------------------------------------------------------------------------ compress
 def _device_compute(sig, tile_size, top_k, energy_thresh, shard):
     from .engine import compress_device
     r = compress_device(sig, tile_size, top_k, energy_thresh=energy_thresh, shard=shard)
@@ -68,9 +120,65 @@ def _device_compute(sig, tile_size, top_k, energy_thresh, shard):
                 n_domains=r.n_domains, silent=r.is_silent)
 
 
+def compress_sharded_device(sig: Optional[torch.Tensor], tile_size: int, top_k: int, energy_thresh: float = 1e-4,
+                            group=None, device: Optional[torch.device] = None, compute: Optional[Callable] = None,
+                            timings: Optional[dict] = None):
+    """The sharded compress on device tensors.  ``sig`` (1-D f32, on ``device``) is needed on rank 0 only.
+    Returns on rank 0 a dict of full-length device tensors idx/s/o/sym/err, the pool, the blocks and geometry;
+    None on the other ranks.  ``timings`` (if given) receives per-phase host seconds (broadcast / compute /
+    gather), each phase closed by a device synchronisation."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    compute = compute or _device_compute
+    tm = timings if timings is not None else {}
+    t0 = time.perf_counter()
+    n_t = torch.zeros(1, dtype=torch.int64, device=device)
+    if rank == 0:
+        n_t[0] = int(sig.numel())
+    _broadcast_(n_t, group, device)
+    n = int(n_t.item())
+    if rank != 0:
+        sig = torch.empty(n, dtype=torch.float32, device=device)
+    _broadcast_(sig, group, device)  # the one data-path collective before the search
+    _sync(device)
+    t1 = time.perf_counter()
+
+    rs, step = geometry(tile_size)
+    nr = -(-n // rs)
+    blocks_box: list = []
+
+    def shard(ranges, n_ranges, range_size):
+        blocks_box[:] = prune_balanced_bounds(ranges, n_ranges, range_size, energy_thresh, world)
+        return blocks_box[rank]
+
+    res = compute(sig, tile_size, top_k, energy_thresh, shard)
+    _sync(device)
+    t2 = time.perf_counter()
+    if res is None:  # empty / short / silent input: identical decision on every rank
+        tm.update(broadcast_s=t1 - t0, compute_s=t2 - t1, gather_s=0.0)
+        return dict(empty=True, n_ranges=0, range_size=rs, domain_step=step, original_len=n) if rank == 0 else None
+    blocks = blocks_box
+    maxlen = max(1, max(b - a for a, b in blocks))
+    cd = _coll_device(group, device)
+    mine = _pack(res, maxlen, cd)
+    glist = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
+    dist.gather(mine, gather_list=glist, dst=0, group=group)
+    _sync(device)
+    t3 = time.perf_counter()
+    tm.update(broadcast_s=t1 - t0, compute_s=t2 - t1, gather_s=t3 - t2)
+    if rank != 0:
+        return None
+    out = _unpack(torch.stack(glist), blocks)
+    silent = res.get("silent")
+    out.update(empty=bool(silent()) if callable(silent) else False, n_ranges=nr, range_size=rs, domain_step=step,
+               original_len=n, pool=res["pool"], blocks=blocks)
+    return out
+
+
 def compress_sharded(signal: Optional[np.ndarray], tile_size: int, top_k: int, energy_thresh: float = 1e-4,
-                     group=None, device: Optional[torch.device] = None,
-                     compute: Optional[Callable] = None):
+                     group=None, device: Optional[torch.device] = None, compute: Optional[Callable] = None):
     """Compress one signal with its ranges split across the ranks of ``group``.
 
     ``signal`` is read on rank 0 only (other ranks may pass None).  Returns, on rank 0, a dict with the
@@ -78,46 +186,192 @@ def compress_sharded(signal: Optional[np.ndarray], tile_size: int, top_k: int, e
     domain_step, original_len, and the per-rank blocks; other ranks return None.
     """
     rank = dist.get_rank(group)
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    sig = None
+    if rank == 0:
+        sig = torch.from_numpy(np.ascontiguousarray(signal, dtype=np.float32)).to(device)
+    out = compress_sharded_device(sig, tile_size, top_k, energy_thresh, group, device, compute)
+    if rank != 0:
+        return None
+    if out.get("empty") and "idx" not in out:
+        return out
+    host = {f: out[f].cpu().numpy() for f in FIELDS}
+    pool = out["pool"]
+    pool = pool.cpu().numpy() if isinstance(pool, torch.Tensor) else np.asarray(pool)
+    host.update({k: v for k, v in out.items() if k not in FIELDS and k != "pool"})
+    host["pool"] = pool.reshape(-1, out["range_size"])
+    return host
+
+
+# ---------------------------------------------------------------------------------------------- decompress
+def decode_span() -> int:
+    from ._lib import size_call
+    return size_call("fwav_decode_span")
+
+
+def decode_bounds(n_ranges: int, world: int, span: Optional[int] = None) -> list[tuple[int, int]]:
+    """Contiguous range blocks on multiples of the decode span (the canonical Δ reduction unit), as even as the
+    span allows.  Decode cost per range is uniform, so no weighting."""
+    span = span or decode_span()
+    nb = -(-n_ranges // span)
+    out = []
+    for r in range(world):
+        a = min(n_ranges, (nb * r // world) * span)
+        b = min(n_ranges, (nb * (r + 1) // world) * span)
+        out.append((a, b))
+    return out
+
+
+class ShardDecoder:
+    """One rank's share of the range-sharded decode on its GPU: the C-ABI sequence fwav_decode_run /
+    fwav_decode_reduce per chunk and fwav_decode_finish (include/fwav.h).  Everything is queued on the current
+    stream; the only host synchronisation is in :meth:`finish`."""
+
+    def __init__(self, idx, s, o, sym, pool, lo, n_ranges_global, range_size, iterations, eps, s_clip=16.0,
+                 s_damping=0.0):
+        from ._lib import size_call
+        self.idx, self.s, self.o, self.sym, self.pool = idx, s, o, sym, pool
+        self.dev = idx.device
+        self.m, self.lo, self.nr, self.rs = int(idx.numel()), int(lo), int(n_ranges_global), int(range_size)
+        self.nd = pool.numel() // self.rs
+        self.iterations, self.eps = int(iterations), float(eps)
+        self.s_clip, self.s_damping = float(abs(np.float32(s_clip))), float(s_damping)
+        ci = size_call("fwav_decode_chunk_iterations")
+        self.n_chunks = -(-self.iterations // ci)
+        self.span = size_call("fwav_decode_span")
+        self.n_prefix = ci * (-(-max(self.nr, 1) // self.span)) * 2
+        self.partials = torch.zeros(size_call("fwav_decode_partials_count", self.nr), dtype=torch.float64,
+                                    device=self.dev)
+        self.a = torch.empty(max(self.m * self.rs, 1), dtype=torch.float32, device=self.dev)
+        self.b = torch.empty(max(self.m * self.rs, 1), dtype=torch.float32, device=self.dev)
+        self.deltas = torch.zeros(max(self.iterations, 1), dtype=torch.float64, device=self.dev)
+        self.state = torch.zeros(4, dtype=torch.int32, device=self.dev)
+
+    def _st(self):
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def _common(self):
+        return (self.idx.data_ptr(), self.s.data_ptr(), self.o.data_ptr(), self.sym.data_ptr(), self.m, self.lo,
+                self.nr, self.rs, self.pool.data_ptr(), self.nd, self.iterations)
+
+    def run(self, chunk: int) -> None:
+        from ._lib import call
+        call("fwav_decode_run", *self._common(), chunk, self.s_clip, self.s_damping, self.a.data_ptr(),
+             self.b.data_ptr(), self.partials.data_ptr(), self.state.data_ptr(), self._st())
+
+    def partials_prefix(self) -> torch.Tensor:
+        """The block partials the ranks all-reduce (SUM) between run() and reduce()."""
+        return self.partials[:self.n_prefix]
+
+    def reduce(self, chunk: int) -> None:
+        from ._lib import call
+        call("fwav_decode_reduce", self.partials.data_ptr(), self.nr, self.iterations, chunk, self.eps,
+             self.deltas.data_ptr(), self.state.data_ptr(), self._st())
+
+    def finish(self):
+        """→ (local reconstruction f32[m·rs] device tensor, iterations run, deltas list)."""
+        from ._lib import call
+        if self.iterations == 0 or self.nr == 0:
+            return torch.zeros(self.m * self.rs, dtype=torch.float32, device=self.dev), 0, []
+        call("fwav_decode_finish", *self._common(), self.s_clip, self.s_damping, self.a.data_ptr(),
+             self.b.data_ptr(), self.state.data_ptr(), self._st())
+        st = self.state.cpu().numpy()
+        ran = int(st[1])
+        out = self.b if int(st[2]) == 1 else self.a
+        return out[:self.m * self.rs], ran, self.deltas.cpu().numpy()[:ran].tolist()
+
+
+def _all_reduce_sum_(t: torch.Tensor, group, device: torch.device) -> None:
+    cd = _coll_device(group, device)
+    if t.device == cd:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        return
+    buf = t.to(cd)
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    t.copy_(buf)
+
+
+def decode_shard(decoder, group=None, device: Optional[torch.device] = None):
+    """Drive one rank's decoder through the chunk loop with the per-chunk all-reduce of Δ partials."""
+    device = device or decoder.dev
+    for c in range(decoder.n_chunks):
+        decoder.run(c)
+        _all_reduce_sum_(decoder.partials_prefix(), group, device)
+        decoder.reduce(c)
+    return decoder.finish()
+
+
+def decompress_sharded(matches_soa: Optional[dict], domains: Optional[np.ndarray], n_ranges: int, range_size: int,
+                       iterations: int = 8, convergence_eps: float = 1e-3, s_clip: float = 16.0,
+                       s_damping: float = 0.0, original_len: Optional[int] = None, group=None,
+                       device: Optional[torch.device] = None, decoder: Optional[Callable] = None,
+                       timings: Optional[dict] = None, span: Optional[int] = None):
+    """decompress_audio (fractal.py:1378-1473) with the ranges split across the ranks of ``group``.
+
+    ``matches_soa`` ({idx, s, o, sym} arrays) and ``domains`` ([n_domains, range_size] f32) are read on rank 0 only.
+    Returns on rank 0 ``(recon numpy f32, info)`` with info = {iterations, deltas, blocks}; None elsewhere.
+    ``decoder`` (tests) builds the rank-local decoder; the default is :class:`ShardDecoder` on the rank's GPU, whose
+    shard bounds must sit on multiples of ``fwav_decode_span()`` (``span`` overrides it for a test decoder)."""
+    rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
-    compute = compute or _device_compute
-    n_t = torch.zeros(1, dtype=torch.int64, device=device)
+    tm = timings if timings is not None else {}
+    t0 = time.perf_counter()
+    meta = torch.zeros(3, dtype=torch.int64, device=device)
     if rank == 0:
-        n_t[0] = int(len(signal))
-    dist.broadcast(n_t, src=0, group=group)
-    n = int(n_t.item())
-    sig = torch.empty(n, dtype=torch.float32, device=device)
+        meta[0], meta[1], meta[2] = int(n_ranges), int(np.asarray(domains).shape[0]), int(range_size)
+    _broadcast_(meta, group, device)
+    nr, nd, rs = (int(v) for v in meta.cpu().tolist())
+    pool = torch.empty(max(nd * rs, 1), dtype=torch.float32, device=device)
+    if rank == 0 and nd:
+        pool[:nd * rs].copy_(torch.from_numpy(np.ascontiguousarray(domains, dtype=np.float32).reshape(-1)))
+    _broadcast_(pool, group, device)
+    bounds = decode_bounds(nr, world, span)
+    maxlen = max(1, max(b - a for a, b in bounds))
+    cd = _coll_device(group, device)
+    mine = torch.empty((4, maxlen), dtype=torch.int32, device=cd)
+    slist = None
     if rank == 0:
-        sig.copy_(torch.from_numpy(np.ascontiguousarray(signal, dtype=np.float32)))
-    dist.broadcast(sig, src=0, group=group)  # the one data-path collective before the search
-
-    rs, step = geometry(tile_size)
-    nr = -(-n // rs)
-    blocks = balanced_bounds(approx_active_weights(sig, rs, energy_thresh), world)
-    lo, hi = blocks[rank]
-    res = compute(sig, tile_size, top_k, energy_thresh, (lo, hi))
-    maxlen = max(b - a for a, b in blocks)
-    if res is None:  # empty / short / silent input: identical decision on every rank
-        return dict(empty=True, n_ranges=0, range_size=rs, domain_step=step, original_len=n) if rank == 0 else None
-    mine = _pack(res, max(maxlen, 1), device)
-    allp = torch.empty((world * 5, max(maxlen, 1)), dtype=torch.int32, device=device)
-    dist.all_gather_into_tensor(allp, mine, group=group)
-    allp = allp.view(world, 5, -1)
+        idx = np.asarray(matches_soa["idx"], np.int32)
+        s = np.asarray(matches_soa["s"], np.float32)
+        o = np.asarray(matches_soa["o"], np.float32)
+        sym = np.asarray(matches_soa["sym"]).astype(np.int32)
+        slist = []
+        for a, b in bounds:
+            p = np.zeros((4, maxlen), np.int32)
+            p[0, :b - a] = idx[a:b]
+            p[1, :b - a] = s[a:b].view(np.int32)
+            p[2, :b - a] = o[a:b].view(np.int32)
+            p[3, :b - a] = sym[a:b]
+            slist.append(torch.from_numpy(p).to(cd))
+    dist.scatter(mine, scatter_list=slist, src=0, group=group)
+    lo, hi = bounds[rank]
+    m = hi - lo
+    mine = mine.to(device)
+    idx_l = mine[0, :m].contiguous()
+    s_l = mine[1, :m].contiguous().view(torch.float32)
+    o_l = mine[2, :m].contiguous().view(torch.float32)
+    sym_l = mine[3, :m].to(torch.uint8)
+    _sync(device)
+    t1 = time.perf_counter()
+    make = decoder or ShardDecoder
+    dec = make(idx_l, s_l, o_l, sym_l, pool[:max(nd * rs, 1)], lo, nr, rs, iterations, convergence_eps, s_clip,
+               s_damping)
+    rec, ran, deltas = decode_shard(dec, group, device)
+    _sync(device)
+    t2 = time.perf_counter()
+    buf = torch.zeros(maxlen * rs, dtype=torch.float32, device=cd)
+    buf[:m * rs] = rec[:m * rs].to(cd)
+    glist = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gather_list=glist, dst=0, group=group)
+    _sync(device)
+    t3 = time.perf_counter()
+    tm.update(distribute_s=t1 - t0, decode_s=t2 - t1, gather_s=t3 - t2)
     if rank != 0:
         return None
-    allp = allp.cpu()
-    parts = {f: [] for f in FIELDS}
-    for r, (a, b) in enumerate(blocks):
-        m = b - a
-        parts["idx"].append(allp[r, 0, :m].numpy().astype(np.int32))
-        parts["s"].append(allp[r, 1, :m].numpy().view(np.float32))
-        parts["o"].append(allp[r, 2, :m].numpy().view(np.float32))
-        parts["sym"].append(allp[r, 3, :m].numpy().astype(np.uint8))
-        parts["err"].append(allp[r, 4, :m].numpy().view(np.float32))
-    out = {f: np.concatenate(v) for f, v in parts.items()}
-    pool = res["pool"]
-    pool = pool.cpu().numpy() if isinstance(pool, torch.Tensor) else np.asarray(pool)
-    out.update(empty=bool(res["silent"]()) if callable(res.get("silent")) else False, n_ranges=nr, range_size=rs,
-               domain_step=step, original_len=n, pool=pool.reshape(-1, rs), blocks=blocks)
-    return out
+    out = torch.cat([glist[r][:(b - a) * rs] for r, (a, b) in enumerate(bounds)]).cpu().numpy()
+    if original_len is not None:
+        out = out[:original_len]
+    return out, dict(iterations=ran, deltas=deltas, blocks=bounds)

@@ -118,7 +118,8 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
     """Run the compress hot path on ``sig`` (1-D float32 tensor on a HIP device).
 
     ``shard=(lo, hi)`` restricts candidate search and the affine solve to ranges ``[lo, hi)`` (the
-    multi-GPU path); voiced detection, pool and embeddings are always computed for the whole signal,
+    multi-GPU path; a callable ``shard(ranges, n_ranges, range_size) -> (lo, hi)`` picks them once the voiced-masked
+    ranges exist); voiced detection, pool and embeddings are always computed for the whole signal,
     because query vectors are domain-embedding rows (quirk Q1) and the voiced state is a scan over the
     whole signal.  Raises ValueError for the reference's own error cases (empty input; n_ranges >
     n_domains).  ``on_pool(pool)``, when given, is called right after the pool kernel is queued (the API
@@ -162,6 +163,8 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
         if res.is_silent() or n < tile_size:
             return _empty(n, rs, tile_size, step, energy_thresh, k)
         raise ValueError("mmap length is greater than file size")  # quirk Q9 (fractal.py:1190-1195)
+    if callable(shard):  # multi-GPU: bounds chosen from the ranges themselves (fwav.dist balances the prune)
+        shard = shard(ranges, nr, rs)
     lo, hi = (0, nr) if shard is None else (int(shard[0]), int(shard[1]))
     if not (0 <= lo <= hi <= nr):
         raise ValueError(f"bad shard {shard} for {nr} ranges")
@@ -215,7 +218,7 @@ def decompress_device(idx: torch.Tensor, s: torch.Tensor, o: torch.Tensor, sym: 
                       n_ranges: int, range_size: int, iterations: int = 8, convergence_eps: float = 1e-3,
                       s_clip: float = 16.0, s_damping: float = 0.0):
     """decompress_audio's loop on device.  Returns (recon f32[n_ranges*range_size] tensor, iterations_run,
-    deltas f64 list).  One host synchronisation (to read the iteration count)."""
+    deltas f64 list).  One host synchronisation (to read the iteration count and the result buffer)."""
     dev = idx.device
     st = _stream(dev)
     nr, rs = int(n_ranges), int(range_size)
@@ -224,7 +227,7 @@ def decompress_device(idx: torch.Tensor, s: torch.Tensor, o: torch.Tensor, sym: 
     a = torch.empty(max(nr * rs, 1), dtype=torch.float32, device=dev)
     b = torch.empty(max(nr * rs, 1), dtype=torch.float32, device=dev)
     deltas = torch.zeros(max(it, 1), dtype=torch.float64, device=dev)
-    state = torch.zeros(2, dtype=torch.int32, device=dev)
+    state = torch.zeros(4, dtype=torch.int32, device=dev)
     wsn = size_call("fwav_decode_workspace_size", nr, rs, it)
     ws = torch.empty(max(wsn, 16), dtype=torch.uint8, device=dev)
     call("fwav_decode", idx.data_ptr(), s.data_ptr(), o.data_ptr(), sym.data_ptr(), nr, rs, pool.data_ptr(), nd, it,
@@ -232,7 +235,7 @@ def decompress_device(idx: torch.Tensor, s: torch.Tensor, o: torch.Tensor, sym: 
          deltas.data_ptr(), state.data_ptr(), ws.data_ptr(), wsn, st)
     stt = state.cpu().numpy()
     ran = int(stt[1])
-    out = b if (ran % 2 == 1) else a
+    out = b if int(stt[2]) == 1 else a
     if nr == 0:
         out = a[:0]
     return out[:nr * rs], ran, deltas.cpu().numpy()[:ran].tolist()

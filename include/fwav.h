@@ -109,15 +109,38 @@ int fwav_affine(const float* ranges, int64_t n_ranges, int range_size, const int
                 float* out_err, void* stream);
 
 /* ------------------------------------------------------------------- decompression loop
- * Replaces decompress_audio (fractal.py:1378-1473): all `iterations` launches are queued at once; a device
- * flag stops the work once Δ = ‖next − rec‖/(‖rec‖ or 1) < eps (Δ in f64).  state[0] = converged flag,
- * state[1] = iterations run (t); result in recon_b if t is odd, else recon_a; deltas[0..t) = Δ per
- * iteration.  recon values are bit-exact with the reference. */
+ * Replaces decompress_audio (fractal.py:1378-1473).  recon values are bit-exact with the reference.
+ * fwav_decode runs the whole loop on one device with no host synchronisation: up to 64 iterations per launch
+ * with each range's reconstruction held in registers (range_size <= 32), Δ = ‖next − rec‖/(‖rec‖ or 1) in f64 per
+ * iteration from fixed-order partial sums, and a device flag that stops the loop at the first Δ < eps.
+ * After the call: state[0] = stopped early, state[1] = iterations run t, state[2] = result buffer (0 → recon_a,
+ * 1 → recon_b), deltas[0..t) = Δ per iteration.  state: int[4]; deltas: f64[iterations]. */
 size_t fwav_decode_workspace_size(int64_t n_ranges, int range_size, int iterations);
 int fwav_decode(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t n_ranges,
                 int range_size, const float* pool, int64_t n_domains, int iterations, double eps, float s_clip,
                 double s_damping, float* recon_a, float* recon_b, double* deltas, int* state, void* workspace,
                 size_t ws_bytes, void* stream);
+
+/* Range-sharded decode (multi-GPU, fwav.dist.decompress_sharded; range_size <= 32).  A rank owns ranges
+ * [lo, lo + m) of n_ranges_global (idx/s/o/sym/recon are the rank's local slices; lo and, unless the shard ends the
+ * signal, m are multiples of fwav_decode_span()).  Per chunk c of fwav_decode_chunk_iterations() iterations:
+ *   fwav_decode_run(c)  → the rank's block partials in partials[0 .. 2·chunk_iterations·ceil(n_ranges_global/span))
+ *                         (other blocks zeroed); the caller all-reduces (SUM) that prefix across ranks;
+ *   fwav_decode_reduce(c) → Δ per iteration and the stop decision, identical on every rank and bit-identical to the
+ *                         single-device fwav_decode (one non-zero contributor per partial, fixed summation order);
+ * then fwav_decode_finish() once.  partials holds fwav_decode_partials_count(n_ranges_global) doubles. */
+int fwav_decode_span(void);
+int fwav_decode_chunk_iterations(void);
+size_t fwav_decode_partials_count(int64_t n_ranges_global);
+int fwav_decode_run(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t m, int64_t lo,
+                    int64_t n_ranges_global, int range_size, const float* pool, int64_t n_domains, int iterations,
+                    int chunk, float s_clip, double s_damping, float* recon_a, float* recon_b, double* partials,
+                    int* state, void* stream);
+int fwav_decode_reduce(const double* partials, int64_t n_ranges_global, int iterations, int chunk, double eps,
+                       double* deltas, int* state, void* stream);
+int fwav_decode_finish(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t m, int64_t lo,
+                       int64_t n_ranges_global, int range_size, const float* pool, int64_t n_domains, int iterations,
+                       float s_clip, double s_damping, float* recon_a, float* recon_b, int* state, void* stream);
 
 #ifdef __cplusplus
 }

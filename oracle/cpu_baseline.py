@@ -7,8 +7,10 @@ extrapolates the full-run compress time the way BASELINE.md §4 prescribes:
 
 with the reference's cost structure: per-domain scipy DCT embedding in one process (fractal.py:271-275),
 per-range sgemv + argpartition in W search processes (fractal.py:1180-1207, 598-630) and a numpy batched
-affine solve (B = 512) in one process running beside them (fractal.py:637-754).  W = the worker processes
-used here (the reference uses cpu_count()//2; the box exposes many more CPUs than its share, so W is capped).
+affine solve (B = 512) in one process running beside them (fractal.py:637-754).  W = the search processes: the
+reference forks cpu_count()//2 (fractal.py:1180-1181), but the GPU box shows the whole machine's CPUs (256) while a
+one-GPU job owns a 16-CPU share, so W is swept over 4/8/16 (capped at the share) and the fastest is reported, with
+the sweep, the CPU model and the host copy bandwidth beside it.
 
 Prints one JSON object on stdout.
 """
@@ -69,7 +71,11 @@ def _search_worker(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
-    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--workers", default=None,
+                    help="search processes, or a comma-separated sweep (default: the reference's cpu_count()//2 "
+                         "capped at the box's CPU share, swept over 4/8/16)")
+    ap.add_argument("--cpu-share", type=int, default=int(os.environ.get("FWAV_CPU_SHARE", "16")),
+                    help="CPUs this job may use (the GPU box gives one GPU a 16-CPU share of a larger machine)")
     ap.add_argument("--search-sample", type=int, default=96, help="ranges per search process")
     ap.add_argument("--embed-sample", type=int, default=16384)
     ap.add_argument("--affine-sample", type=int, default=2048)
@@ -99,17 +105,25 @@ def main():
     act = np.nonzero(~pruned)[0]
     global _EMB
     _EMB = emb_full
-    W = max(1, args.workers)
-    rows = [rng.choice(act, size=args.search_sample, replace=False) for _ in range(W)]
+    ref_w = max(1, (os.cpu_count() or 1) // 2)  # the reference forks cpu_count()//2 search workers (:1180-1181)
+    if args.workers:
+        Ws = sorted({max(1, int(w)) for w in str(args.workers).split(",")})
+    else:
+        Ws = sorted({w for w in (4, 8, 16, ref_w) if w <= max(1, args.cpu_share)} or {1})
+    rows0 = rng.choice(act, size=max(8, args.search_sample // 4), replace=False)
     t0 = time.perf_counter()
-    _search_worker((rows[0][: max(8, args.search_sample // 4)], K))
+    _search_worker((rows0, K))
     t_search_1 = (time.perf_counter() - t0) / max(8, args.search_sample // 4)
     ctx = mp.get_context("fork")
-    t0 = time.perf_counter()
-    with ctx.Pool(W) as p:
-        p.map(_search_worker, [(r, K) for r in rows])
-    wall = time.perf_counter() - t0
-    t_search_w = wall / (W * args.search_sample)  # seconds per range with W processes in parallel
+    sweep = {}
+    for w in Ws:
+        rows_w = [rng.choice(act, size=args.search_sample, replace=False) for _ in range(w)]
+        t0 = time.perf_counter()
+        with ctx.Pool(w) as p:
+            p.map(_search_worker, [(r, K) for r in rows_w])
+        sweep[w] = (time.perf_counter() - t0) / (w * args.search_sample)  # s per range with w processes
+    W = min(sweep, key=sweep.get)
+    t_search_w = sweep[W]
 
     arows = rng.choice(act, size=min(args.affine_sample, len(act)), replace=False)
     cand = O.topk_candidates(emb_full, nr, K, ~np.isin(np.arange(nr), arows))[0][arows]
@@ -121,12 +135,39 @@ def main():
 
     T = t_pool + nd * t_emb + max(len(act) * t_search_w, nr * t_aff)
     sample = (f"{args.config}: full voiced+ranges+pool; embed {len(sel)} domains rowwise; search "
-              f"{W}x{args.search_sample} ranges vs the full {nd}-domain table in {W} processes; affine "
-              f"{len(arows)} ranges; extrapolated to {nr} ranges")
+              f"{W}x{args.search_sample} ranges vs the full {nd}-domain table in {W} processes (best of a sweep "
+              f"over {Ws} processes; the reference would fork cpu_count()//2 = {ref_w}"
+              f"{', capped at this job' + chr(39) + f's {args.cpu_share}-CPU share' if ref_w > args.cpu_share else ''}); affine {len(arows)} ranges; extrapolated to {nr} ranges")
     print(json.dumps(dict(value=nr / T, unit="ranges/s", cores=W, kind="port", sample=sample, extrapolated=True,
                           t_total_s=T, t_pool_s=t_pool, t_embed_per_domain_s=t_emb,
                           t_search_per_range_1proc_s=t_search_1, t_search_per_range_Wproc_s=t_search_w,
-                          t_affine_per_range_s=t_aff, n_ranges=nr, n_domains=nd, cpu_count=os.cpu_count())))
+                          search_sweep_s_per_range={str(k): v for k, v in sweep.items()},
+                          reference_workers=ref_w, cpu_share=args.cpu_share,
+                          t_affine_per_range_s=t_aff, n_ranges=nr, n_domains=nd, cpu_count=os.cpu_count(),
+                          cpu_model=cpu_model(), host_copy_gbs=host_copy_gbs())))
+
+
+def cpu_model() -> str:
+    """The lscpu "Model name" (read from /proc/cpuinfo, which lscpu reports)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.lower().startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_copy_gbs(mb: int = 512, reps: int = 5) -> float:
+    """STREAM-style copy bandwidth of one host thread: (read + write bytes) / time, best of `reps`."""
+    a = np.ones(mb * (1 << 20) // 4, np.float32)
+    b = np.empty_like(a)
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        np.copyto(b, a)
+        best = min(best, time.perf_counter() - t0)
+    return 2 * a.nbytes / best / 1e9
 
 
 if __name__ == "__main__":

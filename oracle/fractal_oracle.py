@@ -344,7 +344,7 @@ def decode(idx, s_st, o_st, sym, pool, n_ranges, range_size, iterations=8, conve
         s_used = np.clip(s_used, -c, c)
         nxt = F32(0.0) + (s_used[:, None] * tiles + o_st[:, None])   # bincount adds into +0.0
         rn = float(np.sqrt(np.sum(recon.astype(np.float64) ** 2)))
-        dn = float(np.sqrt(np.sum((nxt.astype(np.float64) - recon.astype(np.float64)) ** 2)))
+        dn = float(np.sqrt(np.sum((nxt - recon).astype(np.float64) ** 2)))  # f32 difference, as :1460
         delta = dn / (rn if rn > 0 else 1.0)
         recon = nxt
         deltas.append(delta)

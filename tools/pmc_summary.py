@@ -5,7 +5,8 @@ MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7: FETCH_SIZE and WRITE_SI
 (TCC slots), both are in KiB, and on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
 streaming read, so   hbm_bytes = (2 · FETCH_SIZE + WRITE_SIZE) · 1024   per dispatch.
 
-usage: tools/pmc_summary.py --fetch DIR --write DIR --out profiles/pmc_latest.json
+usage: tools/pmc_summary.py --fetch DIR --write DIR --config cfg2 --out profiles/pmc_cfg2.json
+(bench.py reads profiles/pmc_<config>.json for the `traffic` of its own config only)
 DIR = the rocprofv3 -d directory of a `--pmc FETCH_SIZE` (resp. WRITE_SIZE) `--kernel-trace
 --output-format csv` run; every *counter_collection.csv below it is read.
 """
@@ -45,6 +46,8 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--config", required=True, help="bench config the passes ran (cfg2, cfg3, ...)")
+    ap.add_argument("--source", default="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py")
     a = ap.parse_args()
     fe = per_kernel(a.fetch, "FETCH_SIZE")
     wr = per_kernel(a.write, "WRITE_SIZE")
@@ -55,7 +58,7 @@ def main():
         kernels[short(k)] = {"dispatches": len(fe.get(k, [])), "fetch_kib_raw": f, "write_kib": w,
                              "hbm_bytes_per_launch": (2.0 * f + w) * 1024.0}
     out = {"formula": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per dispatch (gfx950 FETCH_SIZE half-count correction)",
-           "kernels": kernels}
+           "config": a.config, "source": a.source, "kernels": kernels}
     for k, v in kernels.items():
         for pat, key in KEYS.items():
             if pat in k and key not in out:

@@ -2,7 +2,7 @@
 # GPU-box script: GPU tests, the default bench line, the rocprofv3 kernel-stats run of the same bench and the two
 # HBM PMC passes (FETCH_SIZE / WRITE_SIZE in separate runs). Everything lands in gpurun_out/; summarise with
 #   tools/prof_summary.py gpurun_out/prof/run_results.db --csv profiles/rNN_kernel_stats_cfg2.csv
-#   tools/pmc_summary.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --out profiles/pmc_latest.json
+#   tools/pmc_summary.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --config cfg2 --out profiles/pmc_cfg2.json
 # Each GPU step has its own time limit; the script stops at the first failing step.
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
