@@ -12,7 +12,8 @@
 // next reconstruction depends only on its own previous one: the loop couples ranges through Δ alone.  So a
 // thread keeps its ranges' T (gathered once from the pool), T − mean T and the reconstruction in registers and
 // runs up to kDecIters iterations without touching HBM, adding its ‖rec‖² and ‖next − rec‖² contributions to
-// per-iteration f64 partials.  Per chunk of kDecIters iterations:
+// per-iteration f64 partials.  Per chunk of ≤ kDecIters iterations (the first chunk is 2 iterations when eps > 0: with
+// s_damping = 0 the reference's loop stops at iteration 2 (Q5), and a chunk that ends at the stop needs no recompute):
 //   k_decode_run     (grid: one block per kDecSpan ranges) → rec after the chunk + block partials[t][block]
 //   k_decode_sum     (grid: one block per iteration)       → Σ over blocks, fixed order
 //   k_decode_stop    (one wave)                            → Δ_t, first t with Δ_t < eps → state
@@ -35,7 +36,7 @@
 namespace fwav {
 
 constexpr int kDecSpan = 4096;     // ranges per run block: the unit of the canonical Δ reduction
-constexpr int kDecIters = 64;      // iterations per run launch
+constexpr int kDecIters = 64;      // iterations per run launch (at most)
 constexpr int kDecThreads = 256;   // run / sum block size (4 waves)
 constexpr int kDecWaves = kDecThreads / kWave;
 
@@ -75,6 +76,20 @@ __device__ __forceinline__ float pw_reg(const F& f, int n_rt) {
   }
 }
 
+// Chunk plan: chunk 0 covers iterations [0, first), chunk c ≥ 1 covers [first + (c−1)·kDecIters, …) (≤ kDecIters).
+__host__ __device__ inline int dec_first(int iterations, double eps) {
+  return (eps > 0.0 && iterations > 2) ? 2 : kDecIters;
+}
+__host__ __device__ inline int dec_t0(int c, int first) { return c == 0 ? 0 : first + (c - 1) * kDecIters; }
+__host__ __device__ inline int dec_len(int c, int first, int iterations) {
+  const int t0 = dec_t0(c, first);
+  const int n = c == 0 ? first : kDecIters;
+  return n < iterations - t0 ? n : iterations - t0;
+}
+__host__ __device__ inline int dec_nchunks(int iterations, int first) {
+  return iterations <= 0 ? 0 : (iterations <= first ? 1 : 1 + (int)cdiv(iterations - first, kDecIters));
+}
+
 struct DecArgs {
   const int32_t* idx;
   const float* s;
@@ -91,6 +106,7 @@ struct DecArgs {
   int rs;
   int iterations;
   int chunk;
+  int first;          // dec_first(iterations, eps)
   float s_clip;
   float c_keep;
   float c_opt;
@@ -108,14 +124,14 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_run(DecArgs a) {
   if constexpr (FINISH) {
     if (a.state[0] == 0) return;  // ran every iteration: the last chunk's output is the result
     k = a.state[3];
-    t0 = k * kDecIters;
+    t0 = dec_t0(k, a.first);
     nit = a.state[1] - t0;
-    if (nit == min(kDecIters, a.iterations - t0)) return;  // stopped at the chunk's last iteration: already there
+    if (nit == dec_len(k, a.first, a.iterations)) return;  // stopped at the chunk's last iteration: already there
   } else {
     if (a.state[0] != 0) return;
     k = a.chunk;
-    t0 = k * kDecIters;
-    nit = min(kDecIters, a.iterations - t0);
+    t0 = dec_t0(k, a.first);
+    nit = dec_len(k, a.first, a.iterations);
   }
   const float* rin = k == 0 ? nullptr : dec_buf(a, k);
   float* rout = dec_buf(a, k + 1);
@@ -211,11 +227,11 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_run(DecArgs a) {
 // One block per iteration t of the chunk: Σ over the nblk_g block partials in a fixed order → sums[t].
 __global__ __launch_bounds__(kDecThreads) void k_decode_sum(const double* __restrict__ partials, int64_t nblk_g,
                                                             double* __restrict__ sums, const int* __restrict__ state,
-                                                            int chunk, int iterations) {
+                                                            int chunk, int first, int iterations) {
   __shared__ double red[kDecWaves][2];
   if (state[0] != 0) return;
   const int t = blockIdx.x;
-  if (t >= min(kDecIters, iterations - chunk * kDecIters)) return;
+  if (t >= dec_len(chunk, first, iterations)) return;
   const double* p = partials + (int64_t)t * nblk_g * 2;
   double a = 0.0, b = 0.0;
   for (int64_t j = threadIdx.x; j < nblk_g; j += kDecThreads) {
@@ -238,11 +254,11 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_sum(const double* __rest
 }
 
 // Δ_t for the chunk's iterations in order; the first Δ_t < eps stops the loop.
-__global__ void k_decode_stop(const double* __restrict__ sums, int chunk, int iterations, double eps,
+__global__ void k_decode_stop(const double* __restrict__ sums, int chunk, int first, int iterations, double eps,
                               int* __restrict__ state, double* __restrict__ deltas) {
   if (threadIdx.x != 0 || state[0] != 0) return;
-  const int t0 = chunk * kDecIters;
-  const int nit = min(kDecIters, iterations - t0);
+  const int t0 = dec_t0(chunk, first);
+  const int nit = dec_len(chunk, first, iterations);
   for (int t = 0; t < nit; ++t) {
     const double nrm = sqrt(sums[2 * t]);
     const double delta = sqrt(sums[2 * t + 1]) / (nrm > 0.0 ? nrm : 1.0);
@@ -393,8 +409,8 @@ void launch_run(const DecArgs& a, int64_t nblk_local, hipStream_t st) {
 }
 
 DecArgs make_args(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t m, int64_t lo,
-                  int64_t nr_global, int rs, const float* pool, int iterations, int chunk, float s_clip,
-                  double s_damping, float* a, float* b, double* partials, int* state) {
+                  int64_t nr_global, int rs, const float* pool, int iterations, int chunk, double eps,
+                  float s_clip, double s_damping, float* a, float* b, double* partials, int* state) {
   DecArgs d;
   d.idx = idx;
   d.s = s;
@@ -411,6 +427,7 @@ DecArgs make_args(const int32_t* idx, const float* s, const float* o, const uint
   d.rs = rs;
   d.iterations = iterations;
   d.chunk = chunk;
+  d.first = dec_first(iterations, eps);
   d.s_clip = fabsf(s_clip);
   d.c_keep = (float)(1.0 - s_damping);  // Python float (1.0 - d) meets an f32 array (NEP 50)
   d.c_opt = (float)s_damping;
@@ -426,6 +443,7 @@ extern "C" {
 
 int fwav_decode_span(void) { return kDecSpan; }
 int fwav_decode_chunk_iterations(void) { return kDecIters; }
+int fwav_decode_n_chunks(int iterations, double eps) { return dec_nchunks(iterations, dec_first(iterations, eps)); }
 
 size_t fwav_decode_partials_count(int64_t nr_global) {
   return (size_t)(kDecIters * dec_blocks(nr_global) * 2 + kDecIters * 2);
@@ -449,8 +467,8 @@ static int check_common(const void* idx, const void* s, const void* o, const voi
 // Sharded building blocks (the single-device fwav_decode below is exactly this sequence with lo = 0, m = nr).
 int fwav_decode_run(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t m,
                     int64_t lo, int64_t nr_global, int rs, const float* pool, int64_t nd, int iterations, int chunk,
-                    float s_clip, double s_damping, float* recon_a, float* recon_b, double* partials, int* state,
-                    void* stream) {
+                    double eps, float s_clip, double s_damping, float* recon_a, float* recon_b, double* partials,
+                    int* state, void* stream) {
   int rc = check_common(idx, s_in, o_in, sym, pool, recon_a, recon_b, state, m, rs, iterations, "fwav_decode_run");
   if (rc) return rc;
   FWAV_CHECK_ARG(partials, FWAV_ERR_ARG, "fwav_decode_run: null partials");
@@ -458,15 +476,15 @@ int fwav_decode_run(const int32_t* idx, const float* s_in, const float* o_in, co
   FWAV_CHECK_ARG(lo >= 0 && lo % kDecSpan == 0 && lo + m <= nr_global && (lo + m == nr_global || m % kDecSpan == 0),
                  FWAV_ERR_SHAPE, "fwav_decode_run: shard [%lld, %lld) of %lld not aligned to %d ranges",
                  (long long)lo, (long long)(lo + m), (long long)nr_global, kDecSpan);
-  FWAV_CHECK_ARG(chunk >= 0 && (int64_t)chunk * kDecIters < iterations, FWAV_ERR_ARG, "fwav_decode_run: chunk");
+  FWAV_CHECK_ARG(chunk >= 0 && chunk < fwav_decode_n_chunks(iterations, eps), FWAV_ERR_ARG, "fwav_decode_run: chunk");
   (void)nd;
   hipStream_t st = (hipStream_t)stream;
   if (chunk == 0) (void)hipMemsetAsync(state, 0, 4 * sizeof(int), st);
   if (m != nr_global)  // other ranks' blocks must add exactly zero in the all-reduce
     (void)hipMemsetAsync(partials, 0, (size_t)kDecIters * dec_blocks(nr_global) * 2 * sizeof(double), st);
   if (m > 0) {
-    DecArgs d = make_args(idx, s_in, o_in, sym, m, lo, nr_global, rs, pool, iterations, chunk, s_clip, s_damping,
-                          recon_a, recon_b, partials, state);
+    DecArgs d = make_args(idx, s_in, o_in, sym, m, lo, nr_global, rs, pool, iterations, chunk, eps, s_clip,
+                          s_damping, recon_a, recon_b, partials, state);
     launch_run<false>(d, dec_blocks(m), st);
   }
   FWAV_LAUNCH_CHECK("fwav_decode_run");
@@ -476,26 +494,29 @@ int fwav_decode_run(const int32_t* idx, const float* s_in, const float* o_in, co
 int fwav_decode_reduce(const double* partials, int64_t nr_global, int iterations, int chunk, double eps,
                        double* deltas, int* state, void* stream) {
   FWAV_CHECK_ARG(partials && deltas && state, FWAV_ERR_ARG, "fwav_decode_reduce: null pointer");
-  FWAV_CHECK_ARG(chunk >= 0 && (int64_t)chunk * kDecIters < iterations, FWAV_ERR_ARG, "fwav_decode_reduce: chunk");
+  FWAV_CHECK_ARG(chunk >= 0 && chunk < fwav_decode_n_chunks(iterations, eps), FWAV_ERR_ARG,
+                 "fwav_decode_reduce: chunk");
+  const int first = dec_first(iterations, eps);
   hipStream_t st = (hipStream_t)stream;
   const int64_t nb = dec_blocks(nr_global);
   double* sums = (double*)partials + (int64_t)kDecIters * nb * 2;
-  k_decode_sum<<<kDecIters, kDecThreads, 0, st>>>(partials, nb, sums, state, chunk, iterations);
-  k_decode_stop<<<1, kWave, 0, st>>>(sums, chunk, iterations, eps, state, deltas);
+  k_decode_sum<<<kDecIters, kDecThreads, 0, st>>>(partials, nb, sums, state, chunk, first, iterations);
+  k_decode_stop<<<1, kWave, 0, st>>>(sums, chunk, first, iterations, eps, state, deltas);
   FWAV_LAUNCH_CHECK("fwav_decode_reduce");
   return FWAV_OK;
 }
 
 int fwav_decode_finish(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t m,
                        int64_t lo, int64_t nr_global, int rs, const float* pool, int64_t nd, int iterations,
-                       float s_clip, double s_damping, float* recon_a, float* recon_b, int* state, void* stream) {
+                       double eps, float s_clip, double s_damping, float* recon_a, float* recon_b, int* state,
+                       void* stream) {
   int rc = check_common(idx, s_in, o_in, sym, pool, recon_a, recon_b, state, m, rs, iterations, "fwav_decode_finish");
   if (rc) return rc;
   FWAV_CHECK_ARG(rs <= kMaxResidentRs, FWAV_ERR_SHAPE, "fwav_decode_finish: range_size %d > %d", rs, kMaxResidentRs);
   (void)nd;
   hipStream_t st = (hipStream_t)stream;
   if (m > 0 && iterations > 0) {
-    DecArgs d = make_args(idx, s_in, o_in, sym, m, lo, nr_global, rs, pool, iterations, 0, s_clip, s_damping,
+    DecArgs d = make_args(idx, s_in, o_in, sym, m, lo, nr_global, rs, pool, iterations, 0, eps, s_clip, s_damping,
                           recon_a, recon_b, nullptr, state);
     launch_run<true>(d, dec_blocks(m), st);
   }
@@ -524,16 +545,16 @@ int fwav_decode(const int32_t* idx, const float* s_in, const float* o_in, const 
   }
   double* partials = (double*)(((uintptr_t)workspace + 63) & ~(uintptr_t)63);
   if (rs <= kMaxResidentRs) {
-    const int nchunks = (int)cdiv(iterations, kDecIters);
+    const int nchunks = fwav_decode_n_chunks(iterations, eps);
     for (int c = 0; c < nchunks; ++c) {
-      rc = fwav_decode_run(idx, s_in, o_in, sym, nr, 0, nr, rs, pool, nd, iterations, c, s_clip, s_damping, recon_a,
-                           recon_b, partials, state, stream);
+      rc = fwav_decode_run(idx, s_in, o_in, sym, nr, 0, nr, rs, pool, nd, iterations, c, eps, s_clip, s_damping,
+                           recon_a, recon_b, partials, state, stream);
       if (rc) return rc;
       rc = fwav_decode_reduce(partials, nr, iterations, c, eps, deltas, state, stream);
       if (rc) return rc;
     }
-    return fwav_decode_finish(idx, s_in, o_in, sym, nr, 0, nr, rs, pool, nd, iterations, s_clip, s_damping, recon_a,
-                              recon_b, state, stream);
+    return fwav_decode_finish(idx, s_in, o_in, sym, nr, 0, nr, rs, pool, nd, iterations, eps, s_clip, s_damping,
+                              recon_a, recon_b, state, stream);
   }
   // range_size > 32: per-iteration streaming
   (void)hipMemsetAsync(recon_a, 0, (size_t)nr * rs * sizeof(float), st);

@@ -16,6 +16,9 @@
 //   tonal[j]     = f32( Σ_n C[j+1][n]·w[j+1]·x[n] ),  j < min(8, rs−1), zero-padded; ‖·‖ f32, /‖·‖ if > 1e-8
 //   transient[k] = Σ_n C[k][n]·w[n]·f64(x[n] − x[n−1]),  k < min(8, rs); f64 norm; /‖·‖ if > 1e-8; → f32
 // Parity is |Δ| ≤ 1e-6 against the reference goldens (SURVEY Appendix A rule 2).
+// Invariant relied on elsewhere: each head has norm ≤ 1 (normalised, or zero).  The similarity search's fp16 error
+// bound δ (fwav_topk.hip kF16Delta) assumes Σ|q_k d_k| ≤ ‖q‖‖d‖ ≤ 2; a change here that breaks it (e.g. honouring
+// transient_weight) must change δ too.  Checked by tests (test_embedding_heads_at_most_unit_norm, full-size cfg3).
 #include "fwav_common.h"
 #include "../../include/fwav.h"
 

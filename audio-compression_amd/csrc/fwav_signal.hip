@@ -153,32 +153,61 @@ __global__ void k_form_ranges(const float* __restrict__ sig, int64_t n, int fram
   if (mask_out != nullptr && p < n) mask_out[p] = m;
 }
 
-// Σ (signal·mask)² in f64, one partial per block (the silent-input test, fractal.py:1083).
-__global__ void k_weighted_energy(const float* __restrict__ ranges, int64_t n, double* __restrict__ partial) {
-  __shared__ double red[kSignalThreads / kWave];
-  double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    double x = ranges[i];
-    acc += x * x;
+// Σ (signal·mask)² exactly as np.sum evaluates it on the reference's f32 array (fractal.py:1083): squares rounded to
+// f32, numpy's reduction loop over buffers of 8192 elements, each buffer a pairwise_sum (fwav_common.h pw_leaf: 128-
+// element leaves, halves split at n/2 − (n/2)%8), the buffer sums added in order into the f32 accumulator (which
+// starts at 0).  Phase 1: one wave per full buffer — a complete tree of 64 leaves, one leaf per lane, combined by
+// shuffles in the tree's (left + right) order; the last, partial buffer is evaluated by one lane with the general
+// recursion.  Phase 2: one lane adds the buffer sums in order.
+constexpr int kNpBuf = 8192;
+
+__device__ float pw_sq_rec(const float* __restrict__ x, int n) {
+  auto sq = [&](int i) { return x[i] * x[i]; };
+  // depth: 8191 → ≤ 6 halvings to reach ≤ 128
+  return pw_rec<7>(sq, 0, n);
+}
+
+__global__ void k_energy_buffers(const float* __restrict__ x, int64_t n, float* __restrict__ bufsum) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t nb = cdiv(n, kNpBuf);
+  if (b >= nb) return;
+  const int64_t off = b * kNpBuf;
+  const int64_t len = n - off < kNpBuf ? n - off : kNpBuf;
+  if (len < kNpBuf) {  // the partial last buffer: general pairwise recursion, one lane
+    if (lane == 0) bufsum[b] = pw_sq_rec(x + off, (int)len);
+    return;
   }
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int j = 0; j < (int)(blockDim.x / kWave); ++j) s += red[j];
-    partial[blockIdx.x] = s;
+  // full buffer: 8192 = 64 leaves of 128 (every split of 8192 … 256 is exactly in half)
+  const float* leaf = x + off + lane * 128;
+  float v = pw_leaf([&](int i) { return leaf[i] * leaf[i]; }, 0, 128);
+#pragma unroll
+  for (int w = 1; w < 64; w <<= 1) {
+    const float right = __shfl_down(v, w);
+    if ((lane & (2 * w - 1)) == 0) v = v + right;  // node = left half + right half
   }
+  if (lane == 0) bufsum[b] = v;
+}
+
+__global__ void k_energy_chain(const float* __restrict__ bufsum, int64_t nb, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  float acc = 0.0f;
+  for (int64_t b = 0; b < nb; ++b) acc = acc + bufsum[b];
+  out[0] = acc;
 }
 
 // Energy prune + degenerate queries + active list (fractal.py:598-622, quirk Q1/Q3/Q11).
 //   pruned            → cand row all −1
-//   query row all 0   → cand row 0..min(K,nd)−1 (every score is 0: the (score desc, index asc) order)
+//   query row all 0   → every score is 0 and the reference's candidates are whatever order numpy's introselect
+//                       (argpartition) + argsort leave equal keys in (fractal.py:537-541, quirk Q11): the caller
+//                       passes that order once per (n_domains, K) in zero_cand (K entries, −1 padded); NULL gives
+//                       0..min(K,nd)−1
 //   otherwise         → appended to `active` for the similarity search
 // RS > 0: compile-time range size (row in registers, unrolled pairwise sum); RS == 0: runtime rs.
 template <int RS>
 __global__ void k_prune(const float* __restrict__ ranges, int64_t nr, int64_t q_offset, int rs_rt, float thr,
-                        int fast_mode, const float* __restrict__ emb, int64_t nd, int k, int32_t* __restrict__ cand,
+                        int fast_mode, const float* __restrict__ emb, int64_t nd, int k,
+                        const int32_t* __restrict__ zero_cand, int32_t* __restrict__ cand,
                         int32_t* __restrict__ active, int32_t* __restrict__ n_active) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nr) return;
@@ -217,7 +246,11 @@ __global__ void k_prune(const float* __restrict__ ranges, int64_t nr, int64_t q_
   if (pruned) {
     for (int j = 0; j < k; ++j) c[j] = -1;
   } else if (zero) {
-    for (int j = 0; j < k; ++j) c[j] = j < nd ? j : -1;
+    if (zero_cand != nullptr) {
+      for (int j = 0; j < k; ++j) c[j] = zero_cand[j];
+    } else {
+      for (int j = 0; j < k; ++j) c[j] = j < nd ? j : -1;
+    }
   }
   // append the searchable ranges: one counter atomic per wave (not per range), index order kept within a wave
   const bool act = !pruned && !zero;
@@ -276,10 +309,18 @@ int fwav_voiced_ranges(const float* sig, int64_t n, int rs, int frame, int smoot
   return FWAV_OK;
 }
 
-// Block partials of Σ ranges[0:n]² (f64), `nblocks` of them; the host sums them in order.
-int fwav_weighted_energy(const float* ranges, int64_t n, double* partial, int nblocks, void* stream) {
-  FWAV_CHECK_ARG(ranges && partial && n >= 0 && nblocks > 0, FWAV_ERR_ARG, "fwav_weighted_energy: bad args");
-  k_weighted_energy<<<nblocks, kSignalThreads, 0, (hipStream_t)stream>>>(ranges, n, partial);
+size_t fwav_weighted_energy_workspace_size(int64_t n) { return (size_t)(cdiv(n > 0 ? n : 1, kNpBuf) * 4 + 64); }
+
+// np.sum(ranges[0:n] ** 2) in float32, bit-exact (see k_energy_buffers); the result lands in sum[0].
+int fwav_weighted_energy(const float* ranges, int64_t n, float* sum, void* workspace, size_t ws_bytes, void* stream) {
+  FWAV_CHECK_ARG(ranges && sum && n >= 0, FWAV_ERR_ARG, "fwav_weighted_energy: bad args");
+  FWAV_CHECK_ARG(workspace && ws_bytes >= fwav_weighted_energy_workspace_size(n), FWAV_ERR_WORKSPACE,
+                 "fwav_weighted_energy: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nb = cdiv(n, kNpBuf);
+  float* bufsum = (float*)workspace;
+  if (nb > 0) k_energy_buffers<<<cdiv(nb, 4), 256, 0, st>>>(ranges, n, bufsum);
+  k_energy_chain<<<1, 64, 0, st>>>(bufsum, nb, sum);
   FWAV_LAUNCH_CHECK("fwav_weighted_energy");
   return FWAV_OK;
 }
@@ -287,7 +328,8 @@ int fwav_weighted_energy(const float* ranges, int64_t n, double* partial, int nb
 // Ranges [q_offset, q_offset + nr) of the whole signal: ranges/cand/active are shard-local (row i), the
 // query embedding of local range i is emb row q_offset + i.
 int fwav_prune(const float* ranges, int64_t nr, int64_t q_offset, int rs, float prune_thr, int fast_mode,
-               const float* emb, int64_t nd, int k, int32_t* cand, int32_t* active, int32_t* n_active, void* stream) {
+               const float* emb, int64_t nd, int k, const int32_t* zero_cand, int32_t* cand, int32_t* active,
+               int32_t* n_active, void* stream) {
   FWAV_CHECK_ARG(ranges && emb && cand && active && n_active && k > 0, FWAV_ERR_ARG, "fwav_prune: bad args");
   FWAV_CHECK_ARG(q_offset >= 0 && q_offset + nr <= nd, FWAV_ERR_SHAPE,
                  "fwav_prune: query rows past n_domains (query rows are domain rows, quirk Q1)");
@@ -298,8 +340,8 @@ int fwav_prune(const float* ranges, int64_t nr, int64_t q_offset, int rs, float 
   const int64_t grid = cdiv(nr, kSignalThreads);
   switch (rs) {
 #define FWAV_PRUNE(RSV)                                                                                      \
-  k_prune<RSV><<<grid, kSignalThreads, 0, st>>>(ranges, nr, q_offset, rs, prune_thr, fast_mode, emb, nd, k, cand, \
-                                                active, n_active)
+  k_prune<RSV><<<grid, kSignalThreads, 0, st>>>(ranges, nr, q_offset, rs, prune_thr, fast_mode, emb, nd, k,     \
+                                                zero_cand, cand, active, n_active)
     case 4: FWAV_PRUNE(4); break;
     case 8: FWAV_PRUNE(8); break;
     case 16: FWAV_PRUNE(16); break;

@@ -1382,11 +1382,21 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
 
 // Host-side plan: default policy from the device's workgroup slots, or a diagnostic override.
 static int g_plan_rt = -1, g_plan_p = -1;
+// Per-device caches (the caller makes the stream's device current: fwav.engine wraps every call in
+// torch.cuda.device); kMaxDev bounds the device ordinal.
+constexpr int kMaxDev = 64;
+static int current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
+  return dev;
+}
 static void topk_device_slots(int& cus, int& per_cu) {
-  static int c = 0, w = 0;
+  static int cs[kMaxDev] = {0}, ws[kMaxDev] = {0};
+  const int dev = current_device();
+  int& c = cs[dev];
+  int& w = ws[dev];
   if (c == 0) {
-    int dev = 0;
-    if (!(hipGetDevice(&dev) == hipSuccess &&
+    if (!(
           hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false>, 64 * k16Waves, 0) ==
               hipSuccess &&
@@ -1485,10 +1495,11 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     // overflow list on the device (no host sync) and exits at once when it is empty.
 #if FWAV_TOPK_OVF_F32
     const size_t lds = topk_lds_bytes<C>();
-    static bool attr32b = false;
-    if (!attr32b) {
+    static bool attr32b[kMaxDev] = {false};
+    const int dev = current_device();
+    if (!attr32b[dev]) {
       (void)hipFuncSetAttribute((const void*)k_sim_topk_f32<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr32b = true;
+      attr32b[dev] = true;
     }
     k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, ovf_list, n_ovf, q_offset, K, cand);
 #else
@@ -1502,10 +1513,11 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
 #endif
   } else {
     const size_t lds = topk_lds_bytes<C>();
-    static bool attr32 = false;
-    if (!attr32) {
+    static bool attr32[kMaxDev] = {false};  // a function attribute is set per device
+    const int dev = current_device();
+    if (!attr32[dev]) {
       (void)hipFuncSetAttribute((const void*)k_sim_topk_f32<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr32 = true;
+      attr32[dev] = true;
     }
     k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, active, n_active, q_offset, K, cand);
   }

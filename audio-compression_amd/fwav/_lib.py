@@ -25,8 +25,9 @@ SIGNATURES = {
     "fwav_stream_sync": (I32, [P]),
     "fwav_voiced_workspace_size": (SZ, [I64, I32]),
     "fwav_voiced_ranges": (I32, [P, I64, I32, I32, I32, F32, F32, P, I64, P, P, SZ, P]),
-    "fwav_weighted_energy": (I32, [P, I64, P, I32, P]),
-    "fwav_prune": (I32, [P, I64, I64, I32, F32, I32, P, I64, I32, P, P, P, P]),
+    "fwav_weighted_energy_workspace_size": (SZ, [I64]),
+    "fwav_weighted_energy": (I32, [P, I64, P, P, SZ, P]),
+    "fwav_prune": (I32, [P, I64, I64, I32, F32, I32, P, I64, I32, P, P, P, P, P]),
     "fwav_embed_tables": (I32, [I32, P]),
     "fwav_pool_workspace_size": (SZ, [I64, I32, I32, I32]),
     "fwav_pool_embed": (I32, [P, I64, I32, I32, I32, P, P, P, P, P, SZ, P]),
@@ -40,10 +41,11 @@ SIGNATURES = {
     "fwav_decode": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, SZ, P]),
     "fwav_decode_span": (I32, []),
     "fwav_decode_chunk_iterations": (I32, []),
+    "fwav_decode_n_chunks": (I32, [I32, F64]),
     "fwav_decode_partials_count": (SZ, [I64]),
-    "fwav_decode_run": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, I32, F32, F64, P, P, P, P, P]),
+    "fwav_decode_run": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, I32, F64, F32, F64, P, P, P, P, P]),
     "fwav_decode_reduce": (I32, [P, I64, I32, I32, F64, P, P, P]),
-    "fwav_decode_finish": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, F32, F64, P, P, P, P]),
+    "fwav_decode_finish": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P]),
 }
 
 

@@ -238,7 +238,7 @@ class ShardDecoder:
         self.iterations, self.eps = int(iterations), float(eps)
         self.s_clip, self.s_damping = float(abs(np.float32(s_clip))), float(s_damping)
         ci = size_call("fwav_decode_chunk_iterations")
-        self.n_chunks = -(-self.iterations // ci)
+        self.n_chunks = size_call("fwav_decode_n_chunks", self.iterations, self.eps)
         self.span = size_call("fwav_decode_span")
         self.n_prefix = ci * (-(-max(self.nr, 1) // self.span)) * 2
         self.partials = torch.zeros(size_call("fwav_decode_partials_count", self.nr), dtype=torch.float64,
@@ -257,7 +257,7 @@ class ShardDecoder:
 
     def run(self, chunk: int) -> None:
         from ._lib import call
-        call("fwav_decode_run", *self._common(), chunk, self.s_clip, self.s_damping, self.a.data_ptr(),
+        call("fwav_decode_run", *self._common(), chunk, self.eps, self.s_clip, self.s_damping, self.a.data_ptr(),
              self.b.data_ptr(), self.partials.data_ptr(), self.state.data_ptr(), self._st())
 
     def partials_prefix(self) -> torch.Tensor:
@@ -274,7 +274,7 @@ class ShardDecoder:
         from ._lib import call
         if self.iterations == 0 or self.nr == 0:
             return torch.zeros(self.m * self.rs, dtype=torch.float32, device=self.dev), 0, []
-        call("fwav_decode_finish", *self._common(), self.s_clip, self.s_damping, self.a.data_ptr(),
+        call("fwav_decode_finish", *self._common(), self.eps, self.s_clip, self.s_damping, self.a.data_ptr(),
              self.b.data_ptr(), self.state.data_ptr(), self._st())
         st = self.state.cpu().numpy()
         ran = int(st[1])

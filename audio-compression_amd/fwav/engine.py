@@ -65,6 +65,40 @@ def embed_tables(rs: int, device: torch.device) -> torch.Tensor:
     return _TABLES[key]
 
 
+_ZERO_CAND: dict = {}
+
+
+def zero_query_candidates(n_domains: int, top_k: int) -> np.ndarray:
+    """The reference's candidate row for a query whose embedding is all zero (quirk Q11): every score is 0, so the row
+    is the order in which numpy's introselect (``argpartition``) and ``argsort`` leave equal keys —
+    ``range_candidates_from_embedding_emb`` (fractal.py:535-541) evaluated on a zero score vector, padded with −1 by
+    ``pad_candidates`` (fractal.py:544-552).  A K-element constant per (n_domains, K), computed once on the host by
+    the same numpy calls the reference makes (the tie order is numpy's, so it is taken from numpy)."""
+    key = (int(n_domains), int(top_k))
+    if key not in _ZERO_CAND:
+        nd, k = key
+        scores = np.zeros(nd, np.float32)
+        if k >= nd:
+            idx = np.argsort(scores)[::-1].astype(np.int32)
+        else:
+            part = np.argpartition(scores, -k)[-k:]
+            idx = part[np.argsort(scores[part])[::-1]].astype(np.int32)
+        out = np.full(k, -1, np.int32)
+        out[:min(k, len(idx))] = idx[:k]
+        _ZERO_CAND[key] = out
+    return _ZERO_CAND[key]
+
+
+_ZERO_CAND_DEV: dict = {}
+
+
+def _zero_cand_device(n_domains: int, top_k: int, device: torch.device) -> torch.Tensor:
+    key = (int(n_domains), int(top_k), str(device))
+    if key not in _ZERO_CAND_DEV:
+        _ZERO_CAND_DEV[key] = torch.from_numpy(zero_query_candidates(n_domains, top_k)).to(device)
+    return _ZERO_CAND_DEV[key]
+
+
 @dataclasses.dataclass
 class DeviceCompressed:
     """Result of :func:`compress_device`.  Device tensors; ``finalize()`` synchronises once."""
@@ -92,10 +126,11 @@ class DeviceCompressed:
     empty: bool = False
 
     def is_silent(self) -> bool:
-        """Σ(signal·mask)² < 1e-8 (fractal.py:1083); f64 here, f32 pairwise in the reference."""
+        """np.sum((signal·mask)²) < 1e-8 (fractal.py:1083): the device computes numpy's float32 sum bit-exactly, and the
+        comparison is float32 against float32(1e-8) (NEP 50)."""
         if self.energy_partial is None:
             return True
-        return float(np.sum(self.energy_partial.cpu().numpy())) < 1e-8
+        return bool(F32(self.energy_partial.cpu().numpy()[0]) < F32(1e-8))
 
 
 def _mark(ev, name: str, end: bool = False):
@@ -111,10 +146,17 @@ def _empty(n, rs, tile, step, thr, k) -> DeviceCompressed:
     return DeviceCompressed(0, rs, tile, step, thr, n, 0, k, (0, 0), empty=True)
 
 
-def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh: float = 1e-4,
-                    fast_mode: bool = True, s_clip: float = 16.0, shard: Optional[tuple[int, int]] = None,
-                    keep_intermediates: bool = False, events: Optional[dict] = None,
-                    search: str = "f16", on_pool=None) -> DeviceCompressed:
+def compress_device(sig: torch.Tensor, *args, **kwargs) -> DeviceCompressed:
+    """Run the compress hot path on ``sig``'s device (made current for the call: the C ABI's per-device plans and
+    kernel attributes are taken from the current HIP device).  See :func:`_compress_device`."""
+    with torch.cuda.device(sig.device):
+        return _compress_device(sig, *args, **kwargs)
+
+
+def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh: float = 1e-4,
+                     fast_mode: bool = True, s_clip: float = 16.0, shard: Optional[tuple[int, int]] = None,
+                     keep_intermediates: bool = False, events: Optional[dict] = None,
+                     search: str = "f16", on_pool=None) -> DeviceCompressed:
     """Run the compress hot path on ``sig`` (1-D float32 tensor on a HIP device).
 
     ``shard=(lo, hi)`` restricts candidate search and the affine solve to ranges ``[lo, hi)`` (the
@@ -154,8 +196,10 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
     _mark(events, "voiced_ranges")
     call("fwav_voiced_ranges", sig.data_ptr(), n, rs, frame, 5, float(thr32), float(lo32), ranges.data_ptr(), nr,
          None, ws.data_ptr(), ws_n, st)
-    partial = torch.empty(256, dtype=torch.float64, device=dev)
-    call("fwav_weighted_energy", ranges.data_ptr(), n, partial.data_ptr(), 256, st)
+    partial = torch.empty(1, dtype=torch.float32, device=dev)
+    wse = size_call("fwav_weighted_energy_workspace_size", n)
+    wsen = torch.empty(wse, dtype=torch.uint8, device=dev)
+    call("fwav_weighted_energy", ranges.data_ptr(), n, partial.data_ptr(), wsen.data_ptr(), wse, st)
     _mark(events, "voiced_ranges")
     res = DeviceCompressed(nr, rs, tile_size, step, energy_thresh, n, nd, k, (0, nr), energy_partial=partial)
     if n < tile_size or nr > nd:
@@ -195,8 +239,9 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
     err = torch.empty(m, dtype=torch.float32, device=dev)
     if m > 0:
         _mark(events, "prune")
+        zc = _zero_cand_device(nd, k, dev)
         call("fwav_prune", rsh.data_ptr(), m, lo, rs, float(F32(energy_thresh * 0.75)), int(bool(fast_mode)),
-             emb.data_ptr(), nd, k, cand.data_ptr(), active.data_ptr(), n_active.data_ptr(), st)
+             emb.data_ptr(), nd, k, zc.data_ptr(), cand.data_ptr(), active.data_ptr(), n_active.data_ptr(), st)
         _mark(events, "prune")
         _mark(events, "sim_topk")
         wk = size_call("fwav_sim_topk_workspace_size", m, nd, k) if (emb16 is not None or k > 64) else 0
@@ -214,9 +259,15 @@ def compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh
     return res
 
 
-def decompress_device(idx: torch.Tensor, s: torch.Tensor, o: torch.Tensor, sym: torch.Tensor, pool: torch.Tensor,
-                      n_ranges: int, range_size: int, iterations: int = 8, convergence_eps: float = 1e-3,
-                      s_clip: float = 16.0, s_damping: float = 0.0):
+def decompress_device(idx: torch.Tensor, *args, **kwargs):
+    """decompress_audio's loop on ``idx``'s device (made current for the call).  See :func:`_decompress_device`."""
+    with torch.cuda.device(idx.device):
+        return _decompress_device(idx, *args, **kwargs)
+
+
+def _decompress_device(idx: torch.Tensor, s: torch.Tensor, o: torch.Tensor, sym: torch.Tensor, pool: torch.Tensor,
+                       n_ranges: int, range_size: int, iterations: int = 8, convergence_eps: float = 1e-3,
+                       s_clip: float = 16.0, s_damping: float = 0.0):
     """decompress_audio's loop on device.  Returns (recon f32[n_ranges*range_size] tensor, iterations_run,
     deltas f64 list).  One host synchronisation (to read the iteration count and the result buffer)."""
     dev = idx.device

@@ -48,9 +48,10 @@ int fwav_voiced_ranges(const float* sig, int64_t n, int range_size, int frame, i
                        float* ranges, int64_t n_ranges, uint8_t* mask_out, void* workspace, size_t ws_bytes,
                        void* stream);
 
-/* Silent-input test of compress_audio (fractal.py:1083): per-block f64 partial sums of ranges[0:n]² into
- * partial[nblocks]; the caller adds them (f64) and compares with 1e-8. */
-int fwav_weighted_energy(const float* ranges, int64_t n, double* partial, int nblocks, void* stream);
+/* Silent-input test of compress_audio (fractal.py:1083): sum[0] = np.sum(ranges[0:n] ** 2) in float32, bit-exact
+ * (numpy's 8192-element reduction buffers, each a pairwise sum); the caller compares it with float32(1e-8). */
+size_t fwav_weighted_energy_workspace_size(int64_t n);
+int fwav_weighted_energy(const float* ranges, int64_t n, float* sum, void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------- domain pool + embeddings
  * Replaces build_domains_memmap (fractal.py:285-334) and build_domain_embeddings → multi_head_embedding →
@@ -66,11 +67,14 @@ int fwav_pool_embed(const float* sig, int64_t n, int tile, int range_size, int s
 /* ------------------------------------------------------------- energy prune + degenerate queries
  * Replaces the per-range prefix of cpu_worker (fractal.py:598-622) for ranges [q_offset, q_offset + n):
  *   mean(r²) < prune_thr (= float32(0.75·energy_thresh), fast_mode) → cand row all −1;
- *   query embedding (domain row q_offset + i, quirk Q1 fractal.py:1190-1195) all zero → cand row 0..K−1;
+ *   query embedding (domain row q_offset + i, quirk Q1 fractal.py:1190-1195) all zero → every score is 0, and the
+ *     reference's row is the order numpy's argpartition + argsort leave equal keys in (fractal.py:537-541, quirk
+ *     Q11): cand row = zero_cand[0..K) (device, −1 padded; the host computes it once per (n_domains, K) with the
+ *     reference's own numpy calls), or 0..K−1 when zero_cand is NULL;
  *   otherwise local index i is appended to active[] (*n_active, device counter) for fwav_sim_topk. */
 int fwav_prune(const float* ranges, int64_t n, int64_t q_offset, int range_size, float prune_thr, int fast_mode,
-               const float* emb, int64_t n_domains, int k, int32_t* cand, int32_t* active, int32_t* n_active,
-               void* stream);
+               const float* emb, int64_t n_domains, int k, const int32_t* zero_cand, int32_t* cand, int32_t* active,
+               int32_t* n_active, void* stream);
 
 /* ------------------------------------------------------------------- similarity top-K
  * Replaces range_candidates_from_embedding_emb + pad_candidates (fractal.py:535-552, 617-622): for each
@@ -123,7 +127,8 @@ int fwav_decode(const int32_t* idx, const float* s, const float* o, const uint8_
 
 /* Range-sharded decode (multi-GPU, fwav.dist.decompress_sharded; range_size <= 32).  A rank owns ranges
  * [lo, lo + m) of n_ranges_global (idx/s/o/sym/recon are the rank's local slices; lo and, unless the shard ends the
- * signal, m are multiples of fwav_decode_span()).  Per chunk c of fwav_decode_chunk_iterations() iterations:
+ * signal, m are multiples of fwav_decode_span()).  Per chunk c < fwav_decode_n_chunks(iterations, eps) (at most
+ * fwav_decode_chunk_iterations() iterations each; the first is 2 iterations when eps > 0):
  *   fwav_decode_run(c)  → the rank's block partials in partials[0 .. 2·chunk_iterations·ceil(n_ranges_global/span))
  *                         (other blocks zeroed); the caller all-reduces (SUM) that prefix across ranks;
  *   fwav_decode_reduce(c) → Δ per iteration and the stop decision, identical on every rank and bit-identical to the
@@ -131,16 +136,18 @@ int fwav_decode(const int32_t* idx, const float* s, const float* o, const uint8_
  * then fwav_decode_finish() once.  partials holds fwav_decode_partials_count(n_ranges_global) doubles. */
 int fwav_decode_span(void);
 int fwav_decode_chunk_iterations(void);
+int fwav_decode_n_chunks(int iterations, double eps);
 size_t fwav_decode_partials_count(int64_t n_ranges_global);
 int fwav_decode_run(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t m, int64_t lo,
                     int64_t n_ranges_global, int range_size, const float* pool, int64_t n_domains, int iterations,
-                    int chunk, float s_clip, double s_damping, float* recon_a, float* recon_b, double* partials,
-                    int* state, void* stream);
+                    int chunk, double eps, float s_clip, double s_damping, float* recon_a, float* recon_b,
+                    double* partials, int* state, void* stream);
 int fwav_decode_reduce(const double* partials, int64_t n_ranges_global, int iterations, int chunk, double eps,
                        double* deltas, int* state, void* stream);
 int fwav_decode_finish(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t m, int64_t lo,
                        int64_t n_ranges_global, int range_size, const float* pool, int64_t n_domains, int iterations,
-                       float s_clip, double s_damping, float* recon_a, float* recon_b, int* state, void* stream);
+                       double eps, float s_clip, double s_damping, float* recon_a, float* recon_b, int* state,
+                       void* stream);
 
 #ifdef __cplusplus
 }

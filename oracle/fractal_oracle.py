@@ -229,16 +229,36 @@ def range_energy_pruned(ranges: np.ndarray, energy_thresh: float, fast_mode: boo
     return pw_mean(ranges * ranges) < prune_threshold(energy_thresh)
 
 
+def zero_query_candidates(nd: int, k: int) -> np.ndarray:
+    """range_candidates_from_embedding_emb (fractal.py:535-541) + pad_candidates (:544-552) for an all-zero query
+    (quirk Q11): every score is 0, so the row is the order numpy's argpartition/argsort leave equal keys in."""
+    scores = np.zeros(nd, F32)
+    if k >= nd:
+        idx = np.argsort(scores)[::-1]
+    else:
+        part = np.argpartition(scores, -k)[-k:]
+        idx = part[np.argsort(scores[part])[::-1]]
+    out = np.full(k, -1, np.int32)
+    out[:min(k, len(idx))] = idx[:k]
+    return out
+
+
 def topk_candidates(emb: np.ndarray, n_ranges: int, k: int, pruned: np.ndarray, chunk: int = 1024):
     """cpu_worker + range_candidates_from_embedding_emb + pad_candidates (fractal.py:556-632, 535-552).
     Query for range i is domain-embedding row i (quirk Q1, fractal.py:1190-1195).  Scores in float32
-    (a GEMM here, sgemv in the reference: same values up to summation order); ties broken by lower index.
+    (a GEMM here, sgemv in the reference: same values up to summation order); ties broken by lower index,
+    except all-zero queries, whose row is the reference's own tie order (zero_query_candidates, quirk Q11).
     Returns (cand i32[nr, k] −1-padded, kth f32[nr], k1th f32[nr])."""
     nd = emb.shape[0]
     cand = np.full((n_ranges, k), -1, np.int32)
     kth = np.full(n_ranges, np.nan, F32)
     k1th = np.full(n_ranges, np.nan, F32)
-    act = np.nonzero(~pruned[:n_ranges])[0]
+    zero = np.all(emb[:n_ranges] == 0, axis=1) & ~pruned[:n_ranges]
+    if zero.any():
+        cand[zero] = zero_query_candidates(nd, k)
+        kth[zero] = 0
+        k1th[zero] = 0
+    act = np.nonzero(~pruned[:n_ranges] & ~zero)[0]
     kk = min(k, nd)
     for s in range(0, len(act), chunk):
         rows = act[s:s + chunk]

@@ -146,12 +146,20 @@ class CpuChunkDecoder:
         self.m, self.lo, self.nr, self.rs = len(idx), lo, nr, rs
         self.iterations, self.eps = iterations, eps
         self.c, self.damp = abs(F32(s_clip)), s_damping
-        self.n_chunks = -(-iterations // self.CI)
+        self.first = 2 if (eps > 0 and iterations > 2) else self.CI  # fwav_decode.hip dec_first
+        self.n_chunks = 0 if iterations <= 0 else (1 if iterations <= self.first else
+                                                   1 + -(-(iterations - self.first) // self.CI))
         self.nblk = -(-max(nr, 1) // SPAN)
         self.part = torch.zeros(self.CI * self.nblk * 2, dtype=torch.float64)
         self.rec = np.zeros((self.m, rs), F32)
         self.start = self.rec
         self.deltas, self.ran, self.stopped = [], 0, False
+
+    def _t0(self, c):
+        return 0 if c == 0 else self.first + (c - 1) * self.CI
+
+    def _len(self, c):
+        return min(self.first if c == 0 else self.CI, self.iterations - self._t0(c))
 
     def _step(self, rec):
         F32 = np.float32
@@ -172,7 +180,7 @@ class CpuChunkDecoder:
         p = self.part.view(self.CI, self.nblk, 2).numpy()
         blk = (self.lo + np.arange(self.m)) // SPAN
         rec = self.rec
-        for t in range(min(self.CI, self.iterations - chunk * self.CI)):
+        for t in range(self._len(chunk)):
             nxt = self._step(rec)
             np.add.at(p[t, :, 0], blk, (rec.astype(np.float64) ** 2).sum(1))  # sequential, in range order
             np.add.at(p[t, :, 1], blk, ((nxt - rec).astype(np.float64) ** 2).sum(1))
@@ -186,11 +194,11 @@ class CpuChunkDecoder:
         if self.stopped:
             return
         p = self.part.view(self.CI, self.nblk, 2).numpy()
-        for t in range(min(self.CI, self.iterations - chunk * self.CI)):
+        for t in range(self._len(chunk)):
             rn, dn = float(np.sum(p[t, :, 0])), float(np.sum(p[t, :, 1]))
             d = np.sqrt(dn) / (np.sqrt(rn) if rn > 0 else 1.0)
             self.deltas.append(d)
-            self.ran = chunk * self.CI + t + 1
+            self.ran = self._t0(chunk) + t + 1
             if d < self.eps:
                 self.stopped = True
                 rec = self.start

@@ -69,3 +69,42 @@ def test_cli_roundtrip(tmp_path):
     assert "error" not in r and os.path.exists(out / "a.wav.fwav")
     r = main(["decompress", str(out / "a.wav.fwav"), "--out", str(tmp_path / "rec")])
     assert "error" not in r and os.path.exists(tmp_path / "rec" / "a.wav.fwav_recon.wav")
+
+
+@pytest.mark.parametrize("case", ["tone", "sweep"])
+def test_cli_outputs_match_reference(tmp_path, case):
+    """`fractal.py compress IN.wav OUT --tile T` then `decompress` (fractal.py:1491-1546, quirk Q8 directories):
+    the .fwav the CLI writes equals the reference's bytes wherever the tuples agree (header and pool always; every
+    match record whose (idx, sym) agrees — the others are rule-4 equal fits / near-ties), and decompressing the
+    reference's own .fwav through the CLI writes exactly the reference's reconstruction as 16-bit PCM."""
+    from fwav.cli import main
+    from fwav.fwavio import read_wav_mono, write_wav
+    from golden_util import load, match_agreement
+    from oracle.fractal_oracle import HEADER_SIZE
+    g = load(case)
+    p = g["p"]
+    wav = tmp_path / f"{case}.wav"
+    write_wav(str(wav), g["signal"], p["framerate"], p["sampwidth"])
+    sig, fr, sw = read_wav_mono(str(wav))
+    assert bit_equal(sig, g["signal"]) and (fr, sw) == (p["framerate"], p["sampwidth"])
+    r = main(["compress", str(wav), str(tmp_path / "out"), "--tile", str(p["tile"])])
+    assert "error" not in r, r
+    mine = np.frombuffer((tmp_path / "out" / f"{case}.wav.fwav").read_bytes(), np.uint8)
+    ref = g["fwav_32"]  # the CLI uses the module-global K = 32 (quirk Q2)
+    assert len(mine) == len(ref)
+    pool_end = HEADER_SIZE + 32 + g["pool"].size * 4
+    assert np.array_equal(mine[:HEADER_SIZE], ref[:HEADER_SIZE])
+    assert np.array_equal(mine[HEADER_SIZE + 32:pool_end], ref[HEADER_SIZE + 32:pool_end])
+    rec = mine[pool_end:].copy().view(np.dtype([("idx", "<i4"), ("s", "<f4"), ("o", "<f4"), ("sym", "u1"),
+                                                ("err", "<f4")]))
+    exact, _, _, unexplained = match_agreement(rec["idx"], rec["sym"], rec["err"], g, 32)
+    assert not unexplained.any()
+    assert np.array_equal(mine[pool_end:].reshape(-1, 17)[exact], ref[pool_end:].reshape(-1, 17)[exact])
+    # decompress the reference's .fwav with the CLI defaults (--iter 8 --eps 1e-3)
+    fw = tmp_path / f"{case}_ref.fwav"
+    fw.write_bytes(ref.tobytes())
+    r = main(["decompress", str(fw), "--out", str(tmp_path / "rec")])
+    assert "error" not in r, r
+    out, fr2, sw2 = read_wav_mono(str(tmp_path / "rec" / f"{case}_ref.fwav_recon.wav"))
+    expect = g["dec_32"].clip(-32768, 32767).astype(np.int16).astype(np.float32)  # write_wav, sampwidth 2
+    assert (fr2, sw2) == (p["framerate"], 2) and bit_equal(out, expect)

@@ -87,6 +87,9 @@ def test_cfg3_geometry_ranges_pool(cfg3):
         p = O.domain_pool(seg, tile, 16, step)[:2048]
         assert np.array_equal(pool[d0:d0 + 2048].cpu().numpy().view(np.uint32), p.view(np.uint32))
         assert np.abs(emb[d0:d0 + 2048].cpu().numpy() - O.embed(p)).max() <= EMB_TOL_FULLSIZE
+    # the fp16 pre-filter's δ assumes every head of every table row has norm ≤ 1 (fwav_topk.hip kF16Delta)
+    heads = emb.double().view(-1, 2, 8).square().sum(-1).sqrt()
+    assert float(heads.max()) <= 1 + 1e-6
 
 
 def test_cfg3_prune_and_search(cfg3):

@@ -3,7 +3,7 @@ tests/golden/make_golden.py from /root/reference/fractal.py).  Bars: SURVEY.md A
 import numpy as np
 import pytest
 
-from golden_util import CASES, bit_equal, candidate_agreement, load
+from golden_util import CASES, MATCH_FLOOR, bit_equal, candidate_agreement, load, match_agreement
 from oracle import fractal_oracle as O
 
 
@@ -37,8 +37,25 @@ def test_candidates_near_tie_rule(case):
         gold = g[f"cand_{K}"]
         assert np.array_equal(pruned, gold[:, 0] < 0)
         cand, _, _ = O.topk_candidates(g["emb"], len(gold), K, pruned)
-        _, bad = candidate_agreement(cand, gold, g[f"kth_{K}"], g[f"k1th_{K}"], g["emb"][:len(gold)], pruned)
+        _, bad = candidate_agreement(cand, gold, g[f"kth_{K}"], g[f"k1th_{K}"], None, pruned)
         assert not bad.any()
+        zeroq = np.all(g["emb"][:len(gold)] == 0, axis=1) & ~pruned
+        assert np.array_equal(cand[zeroq], gold[zeroq])  # quirk Q11: the reference's own tie order
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_end_to_end_rule4(case):
+    """Oracle candidates → oracle affine: every (idx, sym) that differs from the reference's is an equal fit or a
+    near-tie (Appendix A rule 4), and the agreement rate holds its recorded floor."""
+    g = load(case)
+    p = g["p"]
+    pruned = O.range_energy_pruned(g["ranges"], p["thr"])
+    for K in p["Ks"]:
+        cand, _, _ = O.topk_candidates(g["emb"], len(pruned), K, pruned)
+        idx, s, o, sym, err = O.affine(g["ranges"], cand, g["pool"])
+        exact, _, _, unexplained = match_agreement(idx, sym, err, g, K)
+        assert not unexplained.any()
+        assert exact.mean() >= MATCH_FLOOR[(case, K)]
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -83,3 +100,13 @@ def test_pruned_ranges_emit_domain0_inf():
     pr = g[f"cand_{K}"][:, 0] < 0
     assert pr.any()
     assert np.all(g[f"m_idx_{K}"][pr] == 0) and np.all(np.isinf(g[f"m_err_{K}"][pr]))
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_embedding_heads_at_most_unit_norm(case):
+    """The fp16 pre-filter's error bound δ (fwav_topk.hip kF16Delta) assumes every embedding head — tonal dims 0-7,
+    transient dims 8-15 — has norm ≤ 1 (fractal.py:205-207, 161-163 normalise; zero rows stay zero)."""
+    g = load(case)
+    e = g["emb"].astype(np.float64)
+    for head in (e[:, :8], e[:, 8:]):
+        assert np.sqrt((head ** 2).sum(1)).max() <= 1 + 1e-6
