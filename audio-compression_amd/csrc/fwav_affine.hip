@@ -262,7 +262,13 @@ __device__ __forceinline__ void affine_one(const float (&R)[RS], int64_t r, int3
   }
 }
 
-constexpr int kAffBatch = 4;  // ranges per wave in k_affine_batch
+#ifndef FWAV_AFF_BATCH
+#define FWAV_AFF_BATCH 4
+#endif
+constexpr int kAffBatch = FWAV_AFF_BATCH;  // ranges per wave in k_affine_batch
+#ifndef FWAV_AFF_XCD
+#define FWAV_AFF_XCD 1
+#endif
 
 template <int RS>
 __global__ __launch_bounds__(64 * kAffWaves) void k_affine_batch(const float* __restrict__ ranges, int64_t nr,
@@ -273,7 +279,14 @@ __global__ __launch_bounds__(64 * kAffWaves) void k_affine_batch(const float* __
                                                                  uint8_t* __restrict__ out_sym,
                                                                  float* __restrict__ out_err) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)blockIdx.x * kAffWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // consecutive ranges have largely the same candidates (query i is domain row i, and domains i and i+1 are windows
+  // `step` samples apart), so consecutive blocks run on one XCD and find each other's rows in its L2
+#if FWAV_AFF_XCD
+  const int64_t blk = xcd_block(blockIdx.x, gridDim.x);
+#else
+  const int64_t blk = blockIdx.x;
+#endif
+  const int64_t wave = blk * kAffWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t r0 = wave * kAffBatch;
   if (r0 >= nr) return;
   const bool has = lane < K;

@@ -37,6 +37,15 @@ void set_error(const char* fmt, ...);
   } while (0)
 
 constexpr int kWave = 64;
+constexpr int kXcds = 8;  // MI355X: workgroups are dealt round-robin over 8 XCDs, each with its own 4 MiB L2
+
+// Bijective XCD-aware renumbering of workgroup b of nwg: the blocks that share an XCD (b ≡ x mod 8) get one
+// contiguous run of logical indices, so neighbouring work items — which gather overlapping rows — share an L2
+// (cdna_hip_programming.md §5.5 T1; placement is a speed choice only, never relied on for correctness).
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nwg) {
+  const int64_t x = b % kXcds, q = nwg / kXcds, r = nwg % kXcds;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / kXcds;
+}
 
 __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -98,6 +107,20 @@ __device__ __forceinline__ auto pw_sum_n(const F& f) -> decltype(f(0)) {
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// The reference's f32 similarity score, emb_dom @ q (fractal.py:537), in the order its BLAS evaluates it: numpy's
+// sgemv on the (n_domains, 16) table goes to OpenBLAS sgemv_t, whose 4-column microkernel (Haswell/Zen/SkylakeX)
+// accumulates the 16 products in 8 fma lanes, l_j = fma(d[j+8], q[j+8], d[j]·q[j]), then reduces 256 → 128 bits
+// and adds horizontally: ((l0 + l4) + (l1 + l5)) + ((l2 + l6) + (l3 + l7)).  Measured bit-exact against
+// numpy (OpenBLAS 0.3.29) on every golden table except its last n_domains mod 4 columns, which OpenBLAS scores
+// with a different kernel.  D(k) and Q(k) return the k-th element of the domain row and of the query.
+template <class D, class Q>
+__device__ __forceinline__ float sgemv16(const D& d, const Q& q) {
+  float l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) l[j] = __builtin_fmaf(d(j + 8), q(j + 8), d(j) * q(j));
+  return ((l[0] + l[4]) + (l[1] + l[5])) + ((l[2] + l[6]) + (l[3] + l[7]));
+}
 
 // np.clip(x, -c, c) keeps NaN (comparisons false).
 __device__ __forceinline__ float clip_sym(float x, float c) { return x < -c ? -c : (x > c ? c : x); }

@@ -148,15 +148,22 @@ __global__ void k_embed(const float* __restrict__ src, int64_t nd, int rs, int64
 #pragma unroll
   for (int j = 0; j < 4; ++j) o4[j] = make_float4(out[4 * j], out[4 * j + 1], out[4 * j + 2], out[4 * j + 3]);
   if (emb16 != nullptr) {
-    // fp16 copy for the similarity pre-filter, tiled [chunk of 256][half h][256][8] (fwav_topk.hip)
+    // fp16 copies for the similarity search, tiled [chunk of 256][half h][256][8] (fwav_topk.hip): the high part
+    // x_hi = f16(x) (the stream's pre-filter), then, one table further on, the low part x_lo = f16(x − x_hi)
+    // (the replay's refined score x_hi·y_hi + x_hi·y_lo + x_lo·y_hi)
     const int64_t c = d >> 8, j = d & 255;
+    const int64_t n16 = ((nd + 255) >> 8) * 256 * 16;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-      half8 v;
+      half8 vh, vl;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (_Float16)out[8 * hh + e];
-      *reinterpret_cast<half8*>(emb16 + ((c * 2 + hh) * 256 + j) * 8) = v;
+      for (int e = 0; e < 8; ++e) {
+        vh[e] = (_Float16)out[8 * hh + e];
+        vl[e] = (_Float16)(out[8 * hh + e] - (float)vh[e]);
+      }
+      *reinterpret_cast<half8*>(emb16 + ((c * 2 + hh) * 256 + j) * 8) = vh;
+      *reinterpret_cast<half8*>(emb16 + n16 + ((c * 2 + hh) * 256 + j) * 8) = vl;
     }
   }
 }
@@ -172,6 +179,8 @@ static void launch_embed(const float* src, int64_t nd, int rs, int64_t a, int64_
 using namespace fwav;
 
 extern "C" {
+
+size_t fwav_emb16_elems(int64_t nd) { return (size_t)(2 * ((nd + 255) / 256) * 256 * 16); }
 
 // Host-side f64 tables for fwav_pool_embed: tab[16 * rs] (tonal 8 rows, transient 8 rows).
 int fwav_embed_tables(int rs, double* tab) {
@@ -201,8 +210,8 @@ size_t fwav_pool_workspace_size(int64_t n, int tile, int rs, int step) {
 }
 
 // Domain pool + embedding.  pool: f32[nd*rs], emb: f32[nd*16], tab: device copy of fwav_embed_tables(rs).
-// emb16 (optional): fp16 copy in the tiled layout the similarity search streams,
-// f16[ceil(nd/256)*256*16]; rows past nd are zeroed here.
+// emb16 (optional): fp16 high and low parts in the tiled layout the similarity search streams,
+// f16[fwav_emb16_elems(nd)] = 2 tables of ceil(nd/256)*256*16; rows past nd are zeroed here.
 int fwav_pool_embed(const float* sig, int64_t n, int tile, int rs, int step, const double* tab, float* pool,
                     float* emb, void* emb16, void* workspace, size_t ws_bytes, void* stream) {
   FWAV_CHECK_ARG(sig && pool && emb && tab && tile > 0 && rs > 0 && step > 0, FWAV_ERR_ARG,
@@ -233,10 +242,13 @@ int fwav_pool_embed(const float* sig, int64_t n, int tile, int rs, int step, con
   }
   _Float16* e16 = (_Float16*)emb16;
   if (e16 != nullptr && (nd & 255) != 0) {
-    // zero the padded tail of the last chunk (both halves)
+    // zero the padded tail of the last chunk (both halves of both tables)
     const int64_t c = nd >> 8, j0 = nd & 255;
-    for (int hh = 0; hh < 2; ++hh)
-      (void)hipMemsetAsync(e16 + ((c * 2 + hh) * 256 + j0) * 8, 0, (size_t)(256 - j0) * 8 * sizeof(_Float16), st);
+    const int64_t n16 = ((nd + 255) >> 8) * 256 * 16;
+    for (int tb = 0; tb < 2; ++tb)
+      for (int hh = 0; hh < 2; ++hh)
+        (void)hipMemsetAsync(e16 + tb * n16 + ((c * 2 + hh) * 256 + j0) * 8, 0,
+                             (size_t)(256 - j0) * 8 * sizeof(_Float16), st);
   }
   switch (rs) {
     case 4: launch_embed<4>(src, nd, rs, a, b, tab, pool_out, emb, e16, st); break;

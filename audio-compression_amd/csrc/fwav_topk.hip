@@ -6,21 +6,19 @@
 //   pad_candidates                      :544-552
 //
 // Contract: for every active query q (a range index; its query vector is domain-embedding row q), write
-// the K domains with the largest f32 score  s(q,d) = fma-chain_{k=0..15}(emb[d][k]·emb[q][k])  in order
-// (score desc, index asc), −1-padded when nd < K.  The reference scores with BLAS sgemv, whose summation
-// order differs, so candidate parity is defined up to near-ties (SURVEY Appendix A rule 3).
+// the K domains with the largest f32 score s(q,d) = emb[d]·emb[q] evaluated in the reference's own order (numpy →
+// OpenBLAS sgemv, fwav_common.h sgemv16), in (score desc, index asc) order, −1-padded when nd < K.  With the scores
+// bit-identical to the reference's, candidate sets can differ from it only where exactly equal scores straddle the
+// K-th place (numpy's introselect then picks among them; SURVEY Appendix A rule 3).
 //
 // The n_ranges × n_domains score matrix (4.4e11 entries at cfg2) is never materialised.
-// Workgroup = 4 waves × 32 queries.  Per wave and 32-domain tile:
-//   * MFMA f32 32x32x2 ×8 (k = 16), domains as A rows (staged transposed in LDS, shared by the 4 waves),
-//     queries as B columns (registers for the whole stream): lane l owns query l&31 and 16 domain rows,
-//     so the running threshold θ is ONE register per lane.
-//   * threshold test: max of the lane's 16 scores vs θ (v_max3 tree + 1 compare); only when some lane
-//     passes does the wave append (score, index) keys to that query's LDS buffer (capacity C).
-//   * when a buffer holds more than C − 32 entries the wave sorts it (64-lane bitonic on 64-bit keys),
-//     keeps the top K and sets θ to the K-th score.  Domains stream in increasing index order, so a
-//     later domain whose score equals θ can never displace an earlier one: strict '>' is exact.
-// The chunk for the next iteration is prefetched into registers while the current one is consumed.
+//
+// k_sim_topk_f32 (emb16 == NULL; tests and a reference for the production kernel below): workgroup = 4 waves × 32
+// queries; each 256-domain chunk is staged row-major in LDS and every lane scores its query against 16 domain rows
+// of each 32-domain tile with sgemv16 (VALU), keeps a running threshold θ (one register per lane), and appends
+// (score, index) keys that beat θ to the query's LDS buffer; a nearly full buffer is sorted (64-lane bitonic), cut
+// to its top K and θ set to the K-th score.  Domains stream in increasing index order, so a later domain whose
+// score equals θ can never displace an earlier one: strict '>' is exact.
 #include "fwav_common.h"
 #include "../../include/fwav.h"
 
@@ -116,7 +114,7 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
                                                                int64_t q_offset, int K, int32_t* __restrict__ cand) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t* keys = (uint64_t*)smem;                            // [kTopkQ][C]
-  float* lda = (float*)(keys + (size_t)kTopkQ * C);            // [16][kChunk]
+  float* lda = (float*)(keys + (size_t)kTopkQ * C);            // [kChunk][16] (row-major domain rows)
   int* cnt = (int*)(lda + 16 * kChunk);                        // [kTopkQ]
   float* theta = (float*)(cnt + kTopkQ);                       // [kTopkQ]
 
@@ -133,9 +131,9 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
   const int qi = qbase + ql;
   const int32_t q = qi < n_active ? active[qi] : -1;
 
-  float b[8];
+  float qf[16];  // the whole query vector (sgemv16)
 #pragma unroll
-  for (int s = 0; s < 8; ++s) b[s] = q >= 0 ? emb[((int64_t)q + q_offset) * 16 + 2 * s + h] : 0.0f;
+  for (int k = 0; k < 16; ++k) qf[k] = q >= 0 ? emb[((int64_t)q + q_offset) * 16 + k] : 0.0f;
   float th = q >= 0 ? -INFINITY : INFINITY;  // invalid lanes never append
   if (tid < kTopkQ) {
     cnt[tid] = 0;
@@ -161,22 +159,24 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
   for (int64_t c = 0; c < nchunks; ++c) {
     __syncthreads();  // previous chunk fully consumed (and cnt/theta init visible)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lda[(4 * j + 0) * kChunk + tid] = pf[j].x;
-      lda[(4 * j + 1) * kChunk + tid] = pf[j].y;
-      lda[(4 * j + 2) * kChunk + tid] = pf[j].z;
-      lda[(4 * j + 3) * kChunk + tid] = pf[j].w;
-    }
+    for (int j = 0; j < 4; ++j) reinterpret_cast<float4*>(lda)[tid * 4 + j] = pf[j];
     __syncthreads();
     if (c + 1 < nchunks) load_chunk(c + 1);
     const int64_t dbase = c * kChunk;
 
     for (int t = 0; t < kChunk / 32; ++t) {
-      floatx16 acc = {};
+      // the lane's 16 rows of the tile (the row ↔ domain map of the MFMA tiles: d0 + (r&3) + 8*(r>>2))
+      floatx16 acc;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const float a = lda[(2 * s + h) * kChunk + t * 32 + col];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[s], acc, 0, 0, 0);
+      for (int r = 0; r < 16; ++r) {
+        const float4* row = reinterpret_cast<const float4*>(lda) + (t * 32 + 4 * h + (r & 3) + 8 * (r >> 2)) * 4;
+        float dv[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 v = row[j];
+          dv[4 * j] = v.x; dv[4 * j + 1] = v.y; dv[4 * j + 2] = v.z; dv[4 * j + 3] = v.w;
+        }
+        acc[r] = sgemv16([&](int k) { return dv[k]; }, [&](int k) { return qf[k]; });
       }
       const int64_t d0 = dbase + t * 32 + 4 * h;  // domain of acc[r] = d0 + (r&3) + 8*(r>>2)
       // mask rows past nd
@@ -226,15 +226,19 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
 // ------------------------------------------------------------------ fp16 pre-filter + exact f32 rescoring
 // Same contract and results as k_sim_topk_f32 (the production K ≤ 64 search).
 //
-// Exactness.  Scores are first formed by ONE v_mfma_f32_32x32x16_f16 per 32×32 tile from the fp16 copy of the
-// table.  |s16 − s32| ≤ (2u + u²)·Σ|q_k d_k| + f32 accumulation ≤ 1.9584e-3 (u = 2^-11; Σ|q_k d_k| ≤ ‖q‖‖d‖ ≤ 2, the
-// tonal and transient heads each having norm ≤ 1) < δ = 2.0e-3.  A
-// query's candidate buffer holds (s16 key, index) pairs; a compaction takes S16 = its K-th largest s16 and keeps
-// the band s16 > S16 − 2δ, which contains every domain that can still be in the exact top K (K domains have
-// s32 > S16 − δ), and new domains are filtered against that band.  The final pass rescores the band in f32
-// (fma chain k = 0..15, the f32 MFMA's order), sorts (score desc, index asc) and emits K — identical to the
-// all-f32 kernel whatever the processing order.  A band that would not leave 64 free slots flags the query for
-// the exact-mode relaunch (runs of near-identical tiles: periodic signals, voiced speech).
+// Exactness.  Three scores per (query, domain): s32 the exact f32 score (sgemv16), s16 = ONE
+// v_mfma_f32_32x32x16_f16 of the fp16 high parts (x_hi = f16(x)), shl = s16 + MFMA(d_hi, q_lo) + MFMA(d_lo, q_hi)
+// (x_lo = f16(x − x_hi), f32 accumulation).  |s16 − s32| ≤ (2u + u²)·Σ|q_k d_k| + f32 accumulation ≤ 1.9584e-3
+// (u = 2^-11; Σ|q_k d_k| ≤ ‖q‖‖d‖ ≤ 2, the tonal and transient heads each having norm ≤ 1) < δ = 2.0e-3;
+// |shl − s32| ≤ 3u²·2 + fp16-subnormal low parts (≈ 3e-7) + three MFMAs' f32 accumulation (≤ 48 roundings of ≤ 2,
+// 5.7e-6) + s32's own rounding (≈ 1e-6) < δ' = 1e-5 (measured max 6e-7: tools/micro/hilo_err.hip).
+// The stream scores every tile with s16 only and fires a tile when some s16 > lim − δ − 2δ'; the replay of a fired
+// tile adds the two low-part MFMAs and appends (shl, index) keys with shl > lim to the query's buffer.  A
+// compaction takes S = its K-th largest shl and keeps the band shl > lim = S − 2δ' (K domains have s32 ≥ S − δ', so
+// every exact top-K member has shl ≥ S − 2δ').  The final pass rescores the band in exact f32 (sgemv16), sorts
+// (score desc, index asc) and emits K — identical to the all-f32 kernel whatever the processing order.  A band that
+// would not leave 64 free slots (≥ 192 domains within 2δ' of the K-th: runs of identical tiles, periodic signals)
+// flags the query for the exact-mode relaunch.
 //
 // Geometry.  8 waves × 32 queries per workgroup, two workgroups per CU (4 waves per SIMD).  Lane l owns query
 // l & 31 (the MFMA's B column, in registers for the whole run) and 16 domain rows of each tile.  The fp16
@@ -243,7 +247,7 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
 // half while group g is consumed.  Per chunk a wave issues 8 ds_read_b128 + 8 MFMAs and folds each tile's 16
 // outputs into its own integer-max chain (8 × v_max3 per tile), then takes ballots against its integer filter.
 // Chunks with a firing chain are recorded (chunk, chain mask) and replayed at the window end (every 32 groups;
-// every group during the first 32 chunks) from L2/MALL in batches of 8 tiles: recompute the tile's MFMA,
+// every group during the first 32 chunks) from L2/MALL in batches of 8 tiles: recompute the tile's three MFMAs,
 // append survivors to the query's two-ended global key buffer (C = 256 entries), compact a buffer inline when
 // it is nearly full.
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -256,6 +260,39 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define FWAV_TOPK_DELTA 2.0e-3f
 #endif
 constexpr float kF16Delta = FWAV_TOPK_DELTA;
+// δ' ≥ max |shl − s32| (see "Exactness"); the stream fires a tile when s16 > lim − kStreamMargin
+#ifndef FWAV_TOPK_HLDELTA
+#define FWAV_TOPK_HLDELTA 1.0e-5f
+#endif
+constexpr float kHLDelta = FWAV_TOPK_HLDELTA;
+constexpr float kStreamMargin = kF16Delta + 2.0f * kHLDelta;
+// Search modes (template MODE of k_sim_topk_f16; launched as a chain, each relaunch on the previous pass's overflow
+// list, seeded with its band limits):
+//   kModeS16: band on s16 (width 2δ), keys s16 — no low-part MFMAs in the replays;
+//   kModeHL : band on shl (width 2.5δ'), keys shl — three MFMAs per replayed tile, overflows only on ≥ 192 domains
+//             within ≈ 2δ' of the K-th (runs of identical tiles);
+//   kModeEX : exact keys (sgemv16 on the VALU for rows passing the s16 filter), a compaction keeps exactly the top K,
+//             so nothing can overflow.
+constexpr int kModeS16 = 0, kModeHL = 1, kModeEX = 2;
+// The first pass's mode: S16 (→ HL → EX relaunches) for tables of at most kHLFirstMinDomains domains, HL (→ EX) for
+// larger ones.  Same-box A/B (tools/ab_topk.py, identical outputs): cfg2 (1.3 M domains, noise) S16 20.0–20.1 ms vs
+// HL 20.7–21.0 — its bands never overflow, and HL's three-MFMA replays cost more; cfg3 (6.6 M, speech-like) S16
+// 254–258 ms vs HL 186–189 (30.5 % of the queries overflow the S16 band and are searched again); a cfg4 shard (86 M,
+// noise) S16 1,135 ms vs HL 960.  FWAV_TOPK_FIRST=0/1 forces S16/HL (A/B builds).
+#ifndef FWAV_TOPK_FIRST
+#define FWAV_TOPK_FIRST -1
+#endif
+constexpr int64_t kHLFirstMinDomains = int64_t(1) << 22;
+static int g_first_mode = -1;  // fwav_debug_topk_mode (tests): force S16 / HL
+__host__ inline int first_mode(int64_t nd) {
+  if (g_first_mode >= 0) return g_first_mode;
+  return FWAV_TOPK_FIRST >= 0 ? FWAV_TOPK_FIRST : (nd > kHLFirstMinDomains ? kModeHL : kModeS16);
+}
+// HL replays test the tile's s16 against the current limit before the two low-part MFMAs (A/B at cfg2: 21.38 vs
+// 20.98 ms without — the test lengthens each tile's dependent chain; cfg3 192.8 vs 188.5)
+#ifndef FWAV_TOPK_HLPRE
+#define FWAV_TOPK_HLPRE 0
+#endif
 #ifdef FWAV_TOPK_DEBUG
 // Debug builds only (tools/ab_build.sh … -DFWAV_TOPK_DEBUG=<query>): seeds of every query and an event trace of one.
 __device__ uint32_t g_fwav_dbg[(1 << 20) + (1 << 16)];
@@ -299,9 +336,6 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #endif
 #ifndef FWAV_TOPK_WPE
 #define FWAV_TOPK_WPE 4  // launch bound: waves per SIMD the register allocation must allow
-#endif
-#ifndef FWAV_TOPK_OVF_F32
-#define FWAV_TOPK_OVF_F32 0  // 1: recompute overflowed queries with the all-f32 kernel (the former path)
 #endif
 // Ablation builds (tools/ab_build.sh NAME -DFWAV_TOPK_ABL=<dbg bits>): the production kernel with the given `dbg`
 // bits fixed at compile time — the STATS kernel's counters cost registers (it spills), which skews its timings.
@@ -423,19 +457,8 @@ static_assert((kFifo & (kFifo - 1)) == 0, "the fired-chunk ring needs a power-of
 constexpr int kWarmChunks = FWAV_TOPK_WARM;   // ... and after every group during the first 32 chunks
 
 
-__device__ __forceinline__ float score32(const float* __restrict__ emb, int64_t d, const float (&q)[16]) {
-  const float4* p = reinterpret_cast<const float4*>(emb + d * 16);
-  float acc = 0.0f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float4 v = p[j];
-    acc = __builtin_fmaf(v.x, q[4 * j + 0], acc);
-    acc = __builtin_fmaf(v.y, q[4 * j + 1], acc);
-    acc = __builtin_fmaf(v.z, q[4 * j + 2], acc);
-    acc = __builtin_fmaf(v.w, q[4 * j + 3], acc);
-  }
-  return acc;
-}
+// Component c (a compile-time constant after unrolling) of a float4.
+__device__ __forceinline__ float f4c(const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); }
 
 // Max of the 16 scores of a lane as an int over the float bits (v_max3_i32; a float max would be preceded
 // by canonicalising v_max_f32 x,x on every MFMA output).  For a threshold t >= 0, (int)x > (int)t ⟺ x > t
@@ -469,13 +492,11 @@ struct Topk16SmemT {
   unsigned long long wstat[STATS ? NG : 1][kStats];  // STATS builds only (one row per wave)
 };
 
-// Streaming compaction on fp16-MFMA keys (no f32 rescoring, no table loads, no sort): S16 = the K-th largest
-// s16 in the buffer; every exact top-K member has s16 > S16 − 2δ (K domains have s32 > S16 − δ), so keep that
-// band (unsorted; the final pass rescores and sorts) and filter new domains with it.  S16 is only needed as
-// a lower bound at ~2^-11 resolution, so a greedy bitwise radix select over the top 20 bits of the score key
-// finds T ≤ key(S16) with ballots and scalar popcounts (≈ 80 VALU ops, vs ≈ 1,300 + 264 LDS shuffles for a
-// 256-key bitonic sort).  If the band would not leave 64 free slots the query is flagged (ovf) and later
-// recomputed by the exact f32 kernel.
+// Streaming compaction on shl keys (no f32 rescoring, no table loads, no sort): S = the K-th largest shl in the
+// buffer; every exact top-K member has shl ≥ S − 2δ' (K domains have s32 ≥ S − δ'), so keep the band shl > S − 2.5δ'
+// (unsorted; the final pass rescores and sorts) and filter new domains with it.  A greedy bitwise radix select over
+// the 32 key bits finds key(S) with ballots and scalar popcounts (no sort).  If the band would not leave 64 free
+// slots the query is flagged (ovf) and searched again in exact mode.
 // Key-buffer reads: L2-served (sc1), never a possibly stale L1 copy of a line this wave loaded before its later
 // appends to it.
 __device__ __forceinline__ uint64_t ld_key(const uint64_t* p) {
@@ -488,7 +509,7 @@ __device__ __forceinline__ int two_end_slot(int e, int n0) {
   return e < n0 ? e : C - 1 - (e - n0);
 }
 
-template <int C, class SM>
+template <int C, bool HL, class SM>
 __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0, int n1, SM& sm, int ql, int K,
                                               unsigned long long* stats, int& m_out, float& lim_out) {
   constexpr int E = C / 64;
@@ -507,16 +528,17 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0,
   float lim = -INFINITY;
   if (n >= K) {
     uint32_t T = 0;
-    for (int bit = 31; bit >= 12; --bit) {
+    // HL: full precision; S16: the top 20 key bits (S16 is needed only as a lower bound at ≈ 2^-11 resolution)
+    for (int bit = 31; bit >= (HL ? 0 : 12); --bit) {
       const uint32_t Tc = T | (1u << bit);
       int c = 0;
 #pragma unroll
       for (int j = 0; j < E; ++j) c += __popcll(__ballot(hi[j] >= Tc));
       if (c >= K) T = Tc;
     }
-    lim = key2f(T) - 2.0f * kF16Delta;
+    lim = HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta;
   }
-  // keep: every real entry with s16 > lim, written densely in (j, lane) order
+  // keep: every real entry with shl > lim, written densely in (j, lane) order
   int m = 0;
   int ovf = 0;
 #pragma unroll
@@ -544,7 +566,7 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0,
 }
 
 // Final pass of query ql: rescore its two-ended buffer (sm.cnt entries at the front, sm.cnt1 at the back) in exact
-// f32, sort, emit the top K (to `out`, or for a piece back into kq).  Whole wave.  Every per-query buffer and
+// f32 (sgemv16), sort, emit the top K (to `out`, or for a piece back into kq).  Whole wave.  Every per-query buffer and
 // counter is owned by one wave, so no cross-wave fences are needed; the wave's own appended stores are drained
 // once (vmcnt(0)), then all key loads and all row loads are issued together (two memory round trips in total).
 template <int C, class SM>
@@ -587,14 +609,7 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
       const int j = j0 + jj;
       const int e = j * 64 + lane;
       if (j < E && e < n) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          acc = __builtin_fmaf(row[jj][i].x, qv[4 * i + 0], acc);
-          acc = __builtin_fmaf(row[jj][i].y, qv[4 * i + 1], acc);
-          acc = __builtin_fmaf(row[jj][i].z, qv[4 * i + 2], acc);
-          acc = __builtin_fmaf(row[jj][i].w, qv[4 * i + 3], acc);
-        }
+        const float acc = sgemv16([&](int k) { return f4c(row[jj][k >> 2], k & 3); }, [&](int k) { return qv[k]; });
         v[j] = make_key(acc, dd[jj]);
       }
     }
@@ -670,11 +685,12 @@ __device__ __forceinline__ void compact_exact(uint64_t* __restrict__ kq, int n0,
   kth_out = n >= K ? kth : 0ull;
 }
 
-template <int C, bool STATS, class SM, bool EX = false>
+template <int C, bool STATS, class SM, int MODE>
 __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int& qcnt, int& kept, int64_t dt, int64_t nd,
                                              uint64_t* __restrict__ gkeys, SM& sm, int qg, int K, int upd,
                                              unsigned long long* stats, const float* __restrict__ emb = nullptr,
                                              const float* qv = nullptr, uint64_t* kthp = nullptr) {
+  constexpr bool EX = MODE == kModeEX;
   const int lane = threadIdx.x & 63;
   const int col = lane & 31;
   const int h = lane >> 5;
@@ -697,31 +713,57 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
   int slot = h ? C - 1 - qcnt : qcnt;
   const int step = h ? -1 : 1;
   char* kbase = reinterpret_cast<char*>(gkeys);
-  // EX: the tile's exact f32 scores, by the f32 MFMA in the fixed k = 0..15 order (bitwise the fma chain of the
-  // final rescoring; the layout of `acc`): lane (col, h) feeds domain dt + col, dims 2s + h
-  floatx16 ex = {};
   if constexpr (EX) {
-    // (4 float4 loads of the whole row + selects: 916 vs 894 ms at cfg3)
-    float av[8];
-    const float* rp = emb + (dt + col < nd ? dt + col : nd - 1) * 16 + h;
+    // EX: exact f32 keys (sgemv16, the final pass's score) of the rows whose s16 passes the filter — typically one
+    // or none per lane and tile, so they are computed on the VALU from the rows' f32 embeddings, two rows per lane
+    // and memory round trip, in increasing row order (the order of the stores below)
+    uint32_t pm = 0u;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) av[s] = rp[2 * s];
+    for (int r = 0; r < 16; ++r) pm |= (a[r] > thf ? 1u : 0u) << r;
+    while (__ballot(pm != 0u) != 0ull) {
+      int rr[2];
+      bool on[2];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) ex = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], qv[s], ex, 0, 0, 0);
-  }
+      for (int u = 0; u < 2; ++u) {
+        on[u] = pm != 0u;
+        rr[u] = on[u] ? __builtin_ctz(pm) : 0;
+        if (on[u]) pm &= pm - 1u;
+      }
+      float4 row[2][4];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    if (a[r] > thf) {
-      FWAV_TRACE(sm.qrow[ql], 1u, (uint32_t)dt, (uint32_t)((h << 16) | r), (uint32_t)slot);
-      // f2key, branch-free: negative → ~u, else u | sign.  EX: the exact f32 score (fixed fma chain) instead of s16
-      float sc = a[r];
-      if constexpr (EX) sc = ex[r];
-      const uint32_t u = __float_as_uint(sc);
-      const uint32_t key = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
-      const uint64_t k64 = ((uint64_t)key << 32) | (uint64_t)(nd0 - (uint32_t)((r & 3) + 8 * (r >> 2)));
-      // EX: a domain that does not beat the query's current K-th exact key can never enter its top K (groups of
-      // equal scores — repeated or silent tiles — are decided here, without stores or compactions)
-      if (!EX || k64 > *kthp) {
+      for (int u = 0; u < 2; ++u) {
+        const int64_t d = dt + 4 * h + (rr[u] & 3) + 8 * (rr[u] >> 2);
+        const float4* p = reinterpret_cast<const float4*>(emb + (on[u] ? d : dt) * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) row[u][i] = p[i];
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (on[u]) {
+          const int r = rr[u];
+          FWAV_TRACE(sm.qrow[ql], 1u, (uint32_t)dt, (uint32_t)((h << 16) | r), (uint32_t)slot);
+          const float sc = sgemv16([&](int k) { return f4c(row[u][k >> 2], k & 3); }, [&](int k) { return qv[k]; });
+          const uint32_t uu = __float_as_uint(sc);
+          const uint32_t key = uu ^ ((uint32_t)((int32_t)uu >> 31) | 0x80000000u);
+          const uint64_t k64 = ((uint64_t)key << 32) | (uint64_t)(nd0 - (uint32_t)((r & 3) + 8 * (r >> 2)));
+          // a domain that does not beat the query's current K-th exact key can never enter its top K (groups of
+          // equal scores — repeated or silent tiles — are decided here, without stores or compactions)
+          if (k64 > *kthp) {
+            *reinterpret_cast<uint64_t*>(kbase + (uint32_t)((ql * C + slot) * 8)) = k64;
+            slot += step;
+          }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (a[r] > thf) {
+        FWAV_TRACE(sm.qrow[ql], 1u, (uint32_t)dt, (uint32_t)((h << 16) | r), (uint32_t)slot);
+        // f2key of the shl score, branch-free: negative → ~u, else u | sign
+        const uint32_t u = __float_as_uint(a[r]);
+        const uint32_t key = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+        const uint64_t k64 = ((uint64_t)key << 32) | (uint64_t)(nd0 - (uint32_t)((r & 3) + 8 * (r >> 2)));
         *reinterpret_cast<uint64_t*>(kbase + (uint32_t)((ql * C + slot) * 8)) = k64;
         slot += step;
       }
@@ -749,7 +791,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
       compact_exact<C>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l),
                        __builtin_amdgcn_readlane(qcnt, l + 32), K, m, lim, kth_l);
     else
-      compact16_s16<C>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l),
+      compact16_s16<C, MODE == kModeHL>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l),
                        __builtin_amdgcn_readlane(qcnt, l + 32), sm, qg * 32 + l, K, STATS ? stats : nullptr, m, lim);
     if (col == l) {
       qcnt = h ? 0 : m;  // the kept band is written densely at the front
@@ -802,12 +844,14 @@ __device__ __forceinline__ half8 tile_fragment(const _Float16* __restrict__ emb1
   return *reinterpret_cast<const half8*>(emb16 + ((c * 2 + h) * kChunk + col) * 8 + t * 256);
 }
 
-template <int C, bool STATS, class SM, bool EX = false>
-__device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, half8 b, float thf, int& qcnt,
+template <int C, bool STATS, class SM, int MODE>
+__device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb16, const _Float16* __restrict__ emb16lo,
+                                               half8 b, half8 bl, float thf, int& qcnt,
                                                int& kept, ReplayCursor& cur, int tail, int64_t nd, uint64_t* __restrict__ gkeys,
                                                SM& sm, int qg, int K, int upd, unsigned long long* stats,
                                                const float* __restrict__ emb = nullptr, const float* qv = nullptr,
                                                uint64_t* kthp = nullptr) {
+  constexpr bool HL = MODE == kModeHL;
   const int lane = threadIdx.x & 63;
   const int col = lane & 31;
   const int h = lane >> 5;
@@ -817,10 +861,14 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
 #pragma unroll
     for (int u = 0; u < kReplayBatch; ++u) ct[u] = next_tile(cur, tail, sm.fired[qg]);
     if (ct[0] < 0) break;
-    half8 af[kReplayBatch];
+    half8 af[kReplayBatch], afl[HL ? kReplayBatch : 1];
 #pragma unroll
     for (int u = 0; u < kReplayBatch; ++u)  // unconditional loads (no wait on the spot)
       af[u] = tile_fragment(emb16, ct[u] < 0 ? ct[0] : ct[u], h, col);
+    if constexpr (HL) {  // the low parts of the fired tiles' domains (shl)
+#pragma unroll
+      for (int u = 0; u < kReplayBatch; ++u) afl[u] = tile_fragment(emb16lo, ct[u] < 0 ? ct[0] : ct[u], h, col);
+    }
     if (STATS) {  // time the fragment round trip (timing build only: forces the wait here)
       const unsigned long long t_l0 = __builtin_amdgcn_s_memrealtime();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -829,8 +877,17 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
 #pragma unroll
     for (int u = 0; u < kReplayBatch; ++u) {
       if (ct[u] < 0) break;
-      const floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], b, floatx16{}, 0, 0, 0);
-      thf = append_tile<C, STATS, SM, EX>(acc, thf, qcnt, kept, ct[u], nd, gkeys, sm, qg, K, upd, stats, emb, qv,
+      floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], b, floatx16{}, 0, 0, 0);
+      if constexpr (HL) {
+        // The limit may have risen since the tile fired: refine (shl = s16 + d_hi·q_lo + d_lo·q_hi, f32
+        // accumulation) only if some s16 of the tile can still pass (s16 > lim − δ − 2δ')
+#if FWAV_TOPK_HLPRE
+        if (__ballot(fold16((int)0x80000000, acc) > int_threshold(thf - kStreamMargin)) == 0ull) continue;
+#endif
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl[u], b, acc, 0, 0, 0);
+      }
+      thf = append_tile<C, STATS, SM, MODE>(acc, thf, qcnt, kept, ct[u], nd, gkeys, sm, qg, K, upd, stats, emb, qv,
                                           kthp);
     }
     if (ct[kReplayBatch - 1] < 0) break;
@@ -841,8 +898,8 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
 // Seed of a query's band limit before the stream: the K-th largest s16 among the domains of its own window
 // [qrow − 64, qrow + 64).  Consecutive domains are windows 2 samples apart, so this window holds close matches and
 // its K-th score is far above what the first streamed chunks give; a valid start for the rising limit (K domains
-// have s16 ≥ T, so every exact top-K member has s16 > T − 2δ), it removes the first compactions and ≈ 1/4 of the
-// appends.  The wave's window tiles (6 × 32 domains from a tile-aligned base, read from L2/MALL) are scored with
+// have s16 ≥ T, so s32 ≥ T − δ: every exact top-K member has shl > T − δ − 2δ', and s16 > T − 2δ for the exact
+// mode's s16-scale limit), it removes the first compactions and ≈ 1/4 of the appends.  The wave's window tiles (6 × 32 domains from a tile-aligned base, read from L2/MALL) are scored with
 // the stream's own MFMA, recomputed per radix step (a greedy bitwise select over the non-negative keys, ballots
 // free: each query's two lanes combine their counts by one shuffle).  Returns −∞ when fewer than K window scores
 // are ≥ 0.
@@ -851,6 +908,7 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
 #endif
 constexpr int kSeedHalf = FWAV_TOPK_SEEDHALF;
 constexpr int kSeedTiles = (2 * kSeedHalf + 62) / 32 + 1;  // the wave's 32 windows from a tile-aligned base
+template <int MODE>
 __device__ __forceinline__ float seed_limit(const _Float16* __restrict__ emb16, int64_t nd, half8 b, int64_t qrow,
                                             int64_t wbase, int K) {
   const int lane = threadIdx.x & 63;
@@ -894,7 +952,7 @@ __device__ __forceinline__ float seed_limit(const _Float16* __restrict__ emb16, 
     const int c = count_ge(key2f(Tc));
     T = c >= K ? Tc : T;
   }
-  return ok ? key2f(T) - 2.0f * kF16Delta : -INFINITY;
+  return ok ? (MODE == kModeHL ? key2f(T) - kF16Delta - 2.0f * kHLDelta : key2f(T) - 2.0f * kF16Delta) : -INFINITY;
 }
 
 // NC chunks from the LDS slots as a single unrolled software pipeline over their 8·NC tiles: fragments are read
@@ -971,16 +1029,20 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
   }
 }
 
-template <int C, bool STATS, int W = k16Waves, int G = kGroup, int QS = k16Sets, bool EX = false>
-__global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
+template <int C, bool STATS, int MODE, int W = k16Waves, int G = kGroup, int QS = k16Sets>
+__global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
                                                                 const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
                                                                 const int32_t* __restrict__ n_active_p,
                                                                 int64_t q_offset, int K, int32_t* __restrict__ cand,
                                                                 uint64_t* __restrict__ gkeys_all,
                                                                 int32_t* __restrict__ ovf_list,
-                                                                int32_t* __restrict__ n_ovf, int plan_rt,
+                                                                int32_t* __restrict__ n_ovf,
+                                                                const uint32_t* __restrict__ seeds_in,
+                                                                float seed_shift, int plan_rt,
                                                                 int plan_p, int dbg, unsigned long long* gstats) {
+  constexpr bool EX = MODE == kModeEX;
+  constexpr bool HL = MODE == kModeHL;
   constexpr int NG = W * QS;  // query groups of 32 per workgroup; wave w owns groups w·QS .. w·QS + QS − 1
   constexpr bool ABL = STATS || FWAV_TOPK_ABL != 0;  // ablation bits honoured
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
@@ -1025,12 +1087,14 @@ __global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void 
   // 256 = no group barrier, 512 = fold without ballots, 1024 = MFMA without fold, 4096 = record the workgroup
   // timeline (combinable with the others), 8192 = no seeded band limits
   if (!STATS) dbg = FWAV_TOPK_ABL;  // production: 0; ablation builds (-DFWAV_TOPK_ABL=bits) fix the bits at compile time
-  half8 b[QS];
-  float thf[QS];
+  half8 b[QS], bl[QS];  // the query's fp16 high and low parts (MFMA B operands)
+  float thf[QS];        // band limit: on shl (first pass), on s16 (exact mode)
   int upd[QS];
-  float qv[QS][EX ? 8 : 1];  // EX: this lane's half of the exact query vector, qv[s][i] = q[2i + h]
+  float qv[QS][EX ? 16 : 1];  // EX: the exact query vector (sgemv16 keys)
+  const int64_t n16 = (int64_t)cdiv(nd, kChunk) * kChunk * 16;  // halfs per fp16 table
+  const _Float16* emb16lo = emb16 + n16;
   uint64_t kth[QS];           // EX: the query's current K-th exact key (0 until K entries)
-  float exseed[QS];           // EX: the first pass's band limit at overflow
+  float inseed[QS];           // relaunch: the previous pass's band limit at overflow, in this mode's scale
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     const int ql = (wave * QS + s) * 32 + col;
@@ -1038,6 +1102,7 @@ __global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void 
     const int32_t q = qi < n_active ? active[qi] : -1;
     const int64_t qrow = (int64_t)(q < 0 ? 0 : q) + q_offset;
     b[s] = *reinterpret_cast<const half8*>(emb16 + (((qrow >> 8) * 2 + h) * 256 + (qrow & 255)) * 8);
+    bl[s] = *reinterpret_cast<const half8*>(emb16lo + (((qrow >> 8) * 2 + h) * 256 + (qrow & 255)) * 8);
     upd[s] = (q >= 0 && !(dbg & 1)) ? 1 : 0;
     thf[s] = upd[s] ? -INFINITY : INFINITY;  // slots past n_active never take appends
     if (h == 0) {
@@ -1045,12 +1110,13 @@ __global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void 
       sm.qrow[ql] = qrow;
     }
     kth[s] = 0ull;
-    // EX: active = the overflow list, whose position qi holds this query's seed
-    exseed[s] = EX && q >= 0 ? key2f(reinterpret_cast<const uint32_t*>(n_ovf + 1)[qi]) : -INFINITY;
-    if constexpr (EX) {  // the f32 MFMA's B operand: dims 2i + h of the query
-      const float* qp = emb + qrow * 16 + h;
+    // relaunch: active = the previous pass's overflow list, whose position qi holds this query's seed (that pass's
+    // band limit); seed_shift converts it to this mode's scale (S16 → HL: −(δ + 2δ'); HL → EX: −(δ + 2δ'))
+    inseed[s] = seeds_in != nullptr && q >= 0 ? key2f(seeds_in[qi]) - seed_shift : -INFINITY;
+    if constexpr (EX) {
+      const float* qp = emb + qrow * 16;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) qv[s][i] = qp[2 * i];
+      for (int i = 0; i < 16; ++i) qv[s][i] = qp[i];
     }
   }
 
@@ -1061,7 +1127,7 @@ __global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void 
       // whole wave (MFMA + shuffles); lanes of unused query slots discard the result
       const int64_t wbase =
           (int64_t)((__builtin_amdgcn_readfirstlane((int)sm.qrow[(wave * QS + s) * 32]) - kSeedHalf) >> 5) << 5;
-      const float seed = seed_limit(emb16, nd, b[s], sm.qrow[(wave * QS + s) * 32 + col], wbase, K);
+      const float seed = seed_limit<MODE>(emb16, nd, b[s], sm.qrow[(wave * QS + s) * 32 + col], wbase, K);
       if (upd[s]) thf[s] = seed;
 #ifdef FWAV_TOPK_EXTSEED
       // experiment builds: a host-computed lower bound per active query (gstats reinterpreted as float[n_active])
@@ -1076,10 +1142,10 @@ __global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void 
         gstats[16 + slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb)] = __float_as_uint(seed);
     }
   }
-  if constexpr (EX) {
+  if (seeds_in != nullptr) {
 #pragma unroll
     for (int s = 0; s < QS; ++s)
-      if (upd[s]) thf[s] = fmaxf(thf[s], exseed[s]);
+      if (upd[s]) thf[s] = fmaxf(thf[s], inseed[s]);
   }
   const int nchunks = (int)cdiv(nd, kChunk);  // < 2^31 / 256: chunk arithmetic stays 32-bit (scalar)
   // this item's chunk range [c0, c1) (the whole table unless the block is split)
@@ -1185,7 +1251,7 @@ __global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void 
       if (STATS) stat_add(7, t_b1 - t_b0);
       int thi[QS];
 #pragma unroll
-      for (int s = 0; s < QS; ++s) thi[s] = int_threshold(thf[s]);
+      for (int s = 0; s < QS; ++s) thi[s] = int_threshold(HL ? thf[s] - kStreamMargin : thf[s]);
       const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
       if (c_end - cg == G) {
 #if FWAV_TOPK_STAGGER
@@ -1209,7 +1275,7 @@ __global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void 
 #pragma unroll
         for (int s = 0; s < QS; ++s) {
           if (nfired[s] > cur[s].head || cur[s].rem != 0u)
-            thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, EX>(emb16, b[s], thf[s], qcnt[s], kept[s], cur[s],
+            thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s], qcnt[s], kept[s], cur[s],
                                              nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s]);
         }
         if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
@@ -1238,7 +1304,7 @@ __global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void 
     if (ABL && (dbg & 2)) continue;
     int thi[QS];
 #pragma unroll
-    for (int s = 0; s < QS; ++s) thi[s] = int_threshold(thf[s]);
+    for (int s = 0; s < QS; ++s) thi[s] = int_threshold(HL ? thf[s] - kStreamMargin : thf[s]);
     const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
     if (ABL && (dbg & (512 | 1024)) && c_end - cg == G) {
       // ablations 512: fold without ballots, 1024: MFMA without fold (outputs invalid)
@@ -1274,7 +1340,7 @@ __global__ __launch_bounds__(64 * W, EX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void 
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
         if (nfired[s] > cur[s].head || cur[s].rem != 0u)
-          thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, EX>(emb16, b[s], thf[s], qcnt[s], kept[s], cur[s],
+          thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s], qcnt[s], kept[s], cur[s],
                                            nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s]);
       }
       if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
@@ -1398,7 +1464,7 @@ static void topk_device_slots(int& cus, int& per_cu) {
   if (c == 0) {
     if (!(
           hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false>, 64 * k16Waves, 0) ==
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeS16>, 64 * k16Waves, 0) ==
               hipSuccess &&
           c > 0 && w > 0)) {
       c = 256;  // MI355X: 256 CUs × 2 workgroups
@@ -1465,52 +1531,66 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       return FWAV_ERR_WORKSPACE;
     }
     const size_t keys_bytes = f16_keys_bytes(max_q, nd);
-    int32_t* ovf_list = (int32_t*)((char*)gkeys + keys_bytes);
-    // workspace tail: ovf_list[q], n_ovf, then seeds u32[q] (seeds[i] = f2key of the band limit of ovf_list[i])
-    int32_t* n_ovf = ovf_list + (max_q > 0 ? max_q : 1);
-    (void)hipMemsetAsync(n_ovf, 0, sizeof(int32_t), st);
+    const int64_t q1 = max_q > 0 ? max_q : 1;
+    // workspace tail: two overflow lists, each list[q], count, seeds u32[q] (seeds[i] = f2key of the band limit of
+    // list[i]); the first pass's list is the last block of the workspace
+    int32_t* ovf2 = (int32_t*)((char*)gkeys + keys_bytes);
+    int32_t* n_ovf2 = ovf2 + q1;
+    int32_t* ovf1 = n_ovf2 + 1 + q1;
+    int32_t* n_ovf1 = ovf1 + q1;
+    const uint32_t* seeds1 = reinterpret_cast<const uint32_t*>(n_ovf1 + 1);
+    const uint32_t* seeds2 = reinterpret_cast<const uint32_t*>(n_ovf2 + 1);
+    (void)hipMemsetAsync(n_ovf1, 0, sizeof(int32_t), st);
+    (void)hipMemsetAsync(n_ovf2, 0, sizeof(int32_t), st);
     // Geometry: k16Waves waves × k16Sets query sets of 32 per workgroup.  Measured at cfg2 (W, QS=1): W = 8
     // 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms — an even 4 waves per SIMD beats a fuller last round of workgroups.
     int rt, P;
     host_plan_for(max_q, nd, rt, P);
     const TopkPlan pl = make_plan(max_q, rt, P);
+    const bool stats_first = (stats != nullptr && !(dbg & (1 << 17))) || (dbg & 65535) != 0;
+    const int mode1 = first_mode(nd);
+#define FWAV_FIRST(MODE_, STATS_, DBG_, ST_)                                                                    \
+  k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, 0, st>>>(                                 \
+      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, nullptr, 0.0f, rt, P, DBG_, ST_)
 #ifdef FWAV_TOPK_EXTSEED
-    if (stats != nullptr && dbg == 0)
-      k_sim_topk_f16<k16Cap, false><<<pl.items(), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, 0, stats);
-    else
+    if (stats != nullptr && dbg == 0) {
+      if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
+    } else
 #endif
-    if ((stats != nullptr && !(dbg & (1 << 17))) || (dbg & 65535) != 0)
-      k_sim_topk_f16<k16Cap, true><<<pl.items(), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, dbg & 65535, stats);
-    else
-      k_sim_topk_f16<k16Cap, false><<<pl.items(), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf_list, n_ovf, rt, P, 0, nullptr);
-    if (pl.R > 0)
-      k_merge_pieces<k16Cap><<<cdiv(pl.R * k16QB, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, ovf_list,
-                                                                    n_ovf);
-    // Queries whose fp16 band overflowed the buffer (large groups of near-equal scores: periodic or speech-like
-    // signals) are searched again by the same kernel in exact mode: appends carry exact f32 keys and a compaction
-    // keeps exactly the top K, so nothing can overflow.  The relaunch reads its query list and count from the
-    // overflow list on the device (no host sync) and exits at once when it is empty.
-#if FWAV_TOPK_OVF_F32
-    const size_t lds = topk_lds_bytes<C>();
-    static bool attr32b[kMaxDev] = {false};
-    const int dev = current_device();
-    if (!attr32b[dev]) {
-      (void)hipFuncSetAttribute((const void*)k_sim_topk_f32<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr32b[dev] = true;
+    if (stats_first) {
+      if (mode1 == kModeHL) FWAV_FIRST(kModeHL, true, dbg & 65535, stats);
+      else FWAV_FIRST(kModeS16, true, dbg & 65535, stats);
+    } else {
+      if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, nullptr); else FWAV_FIRST(kModeS16, false, 0, nullptr);
     }
-    k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, ovf_list, n_ovf, q_offset, K, cand);
-#else
-    const TopkPlan pl_ex = make_plan(max_q, 0, 1);
+#undef FWAV_FIRST
+    if (pl.R > 0)
+      k_merge_pieces<k16Cap><<<cdiv(pl.R * k16QB, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, ovf1,
+                                                                    n_ovf1);
+    // Queries whose band overflowed the buffer (large groups of equal or nearly equal scores) are searched again by
+    // the same kernel in a narrower mode, on the device-side overflow list (no host sync; a relaunch exits at once
+    // when its list is empty): after an S16 first pass the HL mode, then the exact mode for what still overflows;
+    // after an HL first pass the exact mode, whose compactions keep exactly the top K, so nothing overflows.
+    const TopkPlan pl_re = make_plan(max_q, 0, 1);
+    const int32_t* ex_in = ovf1;
+    const int32_t* ex_n = n_ovf1;
+    const uint32_t* ex_seeds = seeds1;
+    if (mode1 == kModeS16) {
+      k_sim_topk_f16<k16Cap, false, kModeHL><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, ovf1, n_ovf1, q_offset, K, cand, gkeys, ovf2, n_ovf2, seeds1, kStreamMargin, 0, 1, 0,
+          nullptr);
+      ex_in = ovf2;
+      ex_n = n_ovf2;
+      ex_seeds = seeds2;
+    }
     if (stats != nullptr && (dbg & (1 << 17)))  // diagnostic: counters of the exact-mode relaunch only
-      k_sim_topk_f16<k16Cap, true, k16Waves, kGroup, k16Sets, true><<<pl_ex.items(), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, ovf_list, n_ovf, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, 1, 0, stats);
+      k_sim_topk_f16<k16Cap, true, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, ex_seeds, kStreamMargin, 0, 1, 0,
+          stats);
     else
-      k_sim_topk_f16<k16Cap, false, k16Waves, kGroup, k16Sets, true><<<pl_ex.items(), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, ovf_list, n_ovf, q_offset, K, cand, gkeys, ovf_list, n_ovf, 0, 1, 0, nullptr);
-#endif
+      k_sim_topk_f16<k16Cap, false, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
+          emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, ex_seeds, kStreamMargin, 0, 1, 0,
+          nullptr);
   } else {
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32[kMaxDev] = {false};  // a function attribute is set per device
@@ -1544,7 +1624,7 @@ int fwav_topk_max_k(void) { return 4096; }
 size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   const int64_t q = max_q > 0 ? max_q : 1;
   if (k > 64) return large_workspace_bytes(n_domains, q);
-  return f16_keys_bytes(q, n_domains) + (size_t)(2 * q + 1) * sizeof(int32_t);
+  return f16_keys_bytes(q, n_domains) + 2 * (size_t)(2 * q + 1) * sizeof(int32_t);
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,
@@ -1588,6 +1668,14 @@ int fwav_debug_dump(void* host, size_t bytes, unsigned* n_events) {
   return FWAV_OK;
 }
 #endif
+// Diagnostic override of the first pass's mode: 0 = S16 (→ HL → exact relaunches), 1 = HL (→ exact), −1 = by table
+// size (default).  Every mode returns the same candidates.
+int fwav_debug_topk_mode(int mode) {
+  FWAV_CHECK_ARG(mode >= -1 && mode <= 1, FWAV_ERR_ARG, "fwav_debug_topk_mode: mode outside [-1, 1]");
+  g_first_mode = mode;
+  return FWAV_OK;
+}
+
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.
 int fwav_debug_topk_plan(int rt, int pieces) {

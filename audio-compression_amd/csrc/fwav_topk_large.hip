@@ -2,8 +2,8 @@
 //
 // Replaces the same reference code as fwav_topk.hip for the module-global top_k > 64 (fractal.py:77, 535-552,
 // 544-552), including K >= n_domains (the reference then returns every domain, sorted, −1-padded to K).
-// Same contract: per active query, the K largest f32 scores fma-chain_{k=0..15}(emb[d][k]·q[k]) in
-// (score desc, index asc) order.
+// Same contract: per active query, the K largest f32 scores emb[d]·q in the reference's sgemv order
+// (fwav_common.h sgemv16), in (score desc, index asc) order.
 //
 // Not the benchmark path (K = 64 runs k_sim_topk_f16).  Queries are processed in batches of B: k_scores_batch
 // materialises the B × nd score rows in the workspace (embedding table read once per batch, coalesced row
@@ -30,10 +30,7 @@ constexpr int kScoreQ = 32;            // queries per k_scores_batch pass (q vec
 constexpr size_t kLargeBudget = size_t(1) << 30;  // score-row workspace budget (bytes)
 
 __device__ __forceinline__ float score_chain(const float (&e)[16], const float* __restrict__ q) {
-  float acc = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) acc = __builtin_fmaf(e[k], q[k], acc);
-  return acc;
+  return sgemv16([&](int k) { return e[k]; }, [&](int k) { return q[k]; });
 }
 
 // S[j·nd + d] = score(domain d, query active[qb + j]) for j < B (rows of queries past n_active untouched).

@@ -28,6 +28,7 @@ SIGNATURES = {
     "fwav_weighted_energy_workspace_size": (SZ, [I64]),
     "fwav_weighted_energy": (I32, [P, I64, P, P, SZ, P]),
     "fwav_prune": (I32, [P, I64, I64, I32, F32, I32, P, I64, I32, P, P, P, P, P]),
+    "fwav_emb16_elems": (SZ, [I64]),
     "fwav_embed_tables": (I32, [I32, P]),
     "fwav_pool_workspace_size": (SZ, [I64, I32, I32, I32]),
     "fwav_pool_embed": (I32, [P, I64, I32, I32, I32, P, P, P, P, P, SZ, P]),
@@ -36,6 +37,7 @@ SIGNATURES = {
     "fwav_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, SZ, P]),
     "fwav_debug_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, I32, P, P]),
     "fwav_debug_topk_plan": (I32, [I32, I32]),
+    "fwav_debug_topk_mode": (I32, [I32]),
     "fwav_affine": (I32, [P, I64, I32, P, I32, P, I64, F32, P, P, P, P, P, P]),
     "fwav_decode_workspace_size": (SZ, [I64, I32, I32]),
     "fwav_decode": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, SZ, P]),

@@ -218,7 +218,7 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     emb = torch.empty(nd * 16, dtype=torch.float32, device=dev)
     if search not in ("f16", "f32"):
         raise ValueError("search must be 'f16' (fp16 pre-filter + exact f32 rescoring) or 'f32'")
-    emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device=dev) if search == "f16" else None
+    emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device=dev) if search == "f16" else None
     ws_p = size_call("fwav_pool_workspace_size", n, tile_size, rs, step)
     wsp = torch.empty(max(ws_p, 16), dtype=torch.uint8, device=dev)
     _mark(events, "pool_embed")

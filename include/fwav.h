@@ -57,8 +57,10 @@ int fwav_weighted_energy(const float* ranges, int64_t n, float* sum, void* works
  * Replaces build_domains_memmap (fractal.py:285-334) and build_domain_embeddings → multi_head_embedding →
  * tile_embedding / transient_embedding (fractal.py:238-280, 166-208, 154-164).
  * pool f32[n_domains·range_size] (bit-exact), emb f32[n_domains·16] (|Δ| ≤ 1e-6 vs the reference),
- * emb16 (optional) fp16 copy in the similarity search's tiled layout, f16[ceil(n_domains/256)·256·16].
+ * emb16 (optional) fp16 copies in the search's tiled layout, f16[fwav_emb16_elems(n_domains)]: the high part
+ * f16(emb) then the low part f16(emb − f16(emb)), ceil(n_domains/256)·256·16 halfs each.
  * n_domains = (n − tile) / step + 1.  tab = device copy of fwav_embed_tables(range_size) (host call). */
+size_t fwav_emb16_elems(int64_t n_domains);
 int fwav_embed_tables(int range_size, double* tab_host /* [16·range_size] */);
 size_t fwav_pool_workspace_size(int64_t n, int tile, int range_size, int step);
 int fwav_pool_embed(const float* sig, int64_t n, int tile, int range_size, int step, const double* tab, float* pool,
@@ -102,6 +104,10 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, 
  * ranges, or with pieces == -1 into two query halves (rt < 0 restores the default policy).  Every plan returns the
  * same candidates.  Re-query fwav_sim_topk_workspace_size afterwards. */
 int fwav_debug_topk_plan(int rt, int pieces);
+/* Diagnostic override of the fp16 search's first-pass mode: 0 = fp16 band (overflowing queries relaunched with the
+ * hi/lo band, then exact keys), 1 = hi/lo band (then exact keys), −1 = by table size (the default: hi/lo above 4 Mi
+ * domains).  Every mode returns the same candidates. */
+int fwav_debug_topk_mode(int mode);
 
 /* ------------------------------------------------------------------- batched affine solve
  * Replaces _flush_gpu_batch / _process_gpu_batch (fractal.py:852-870, 757-850): per range, over the K

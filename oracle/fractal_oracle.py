@@ -243,11 +243,54 @@ def zero_query_candidates(nd: int, k: int) -> np.ndarray:
     return out
 
 
-def topk_candidates(emb: np.ndarray, n_ranges: int, k: int, pruned: np.ndarray, chunk: int = 1024):
+def sgemv_scores(emb: np.ndarray, q: np.ndarray) -> np.ndarray:
+    """emb @ q for a block of queries q (R, 16), in the order the reference's BLAS evaluates it (fractal.py:537:
+    numpy sgemv → OpenBLAS sgemv_t 4-column microkernel): l_j = fma(d[j+8], q[j+8], f32(d[j]·q[j])), then
+    ((l0 + l4) + (l1 + l5)) + ((l2 + l6) + (l3 + l7)).  The fma is evaluated in x87 extended precision (the 48-bit
+    product is exact; the one further rounding before f32 is a double rounding only at an exact extended-precision
+    midpoint).  Bit-exact against numpy here except the table's last n_domains mod 4 columns (OpenBLAS's tail
+    kernel).  Returns (R, nd) float32."""
+    E = np.asarray(emb, F32)
+    Q = np.asarray(q, F32)
+    lanes = []
+    for j in range(8):
+        c = Q[:, None, j] * E[None, :, j]                       # f32 product, rounded
+        p = Q[:, None, j + 8].astype(np.float64) * E[None, :, j + 8].astype(np.float64)  # exact
+        lanes.append(fma_f32(p, c.astype(np.float64)))
+    r = [lanes[i] + lanes[i + 4] for i in range(4)]
+    return (r[0] + r[1]) + (r[2] + r[3])
+
+
+def fma_f32(p: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """round_to_f32(p + c) for an exact f64 product p of two f32 and an f32 value c, i.e. f32 fma: s = fl64(p + c)
+    with its exact error e (TwoSum); fl32(s) is the correctly rounded result unless s lies exactly on a midpoint of
+    two f32 neighbours (s is the nearest f64 to p + c, and f32 midpoints are f64 values), where the sign of e
+    decides instead of ties-to-even."""
+    s = p + c
+    bb = s - p
+    e = (p - (s - bb)) + (c - bb)
+    r = s.astype(F32)
+    r64 = r.astype(np.float64)
+    other = np.nextafter(r, np.where(s > r64, np.float32(np.inf), np.float32(-np.inf)).astype(F32))
+    mid = (r64 + other.astype(np.float64)) * 0.5
+    fix = (s == mid) & (e != 0)
+    if fix.any():
+        hi = np.maximum(r, other)
+        lo = np.minimum(r, other)
+        r = np.where(fix, np.where(e > 0, hi, lo), r)
+    return r
+
+
+#: bound on the difference between two f32 summation orders of a 16-term dot product whose Σ|q_k d_k| ≤ 2 (each is
+#: within 15·2^-24·2 ≈ 1.8e-6 of the exact value), with margin
+SGEMV_GAP = 8e-6
+
+
+def topk_candidates(emb: np.ndarray, n_ranges: int, k: int, pruned: np.ndarray, chunk: int = 512):
     """cpu_worker + range_candidates_from_embedding_emb + pad_candidates (fractal.py:556-632, 535-552).
-    Query for range i is domain-embedding row i (quirk Q1, fractal.py:1190-1195).  Scores in float32
-    (a GEMM here, sgemv in the reference: same values up to summation order); ties broken by lower index,
-    except all-zero queries, whose row is the reference's own tie order (zero_query_candidates, quirk Q11).
+    Query for range i is domain-embedding row i (quirk Q1, fractal.py:1190-1195).  Scores in float32 in the
+    reference's sgemv order (sgemv_scores); ties broken by lower index, except all-zero queries, whose row is the
+    reference's own tie order (zero_query_candidates, quirk Q11).
     Returns (cand i32[nr, k] −1-padded, kth f32[nr], k1th f32[nr])."""
     nd = emb.shape[0]
     cand = np.full((n_ranges, k), -1, np.int32)
@@ -260,21 +303,28 @@ def topk_candidates(emb: np.ndarray, n_ranges: int, k: int, pruned: np.ndarray, 
         k1th[zero] = 0
     act = np.nonzero(~pruned[:n_ranges] & ~zero)[0]
     kk = min(k, nd)
+    E = np.asarray(emb, F32)
     for s in range(0, len(act), chunk):
         rows = act[s:s + chunk]
-        sc = emb[rows] @ emb.T
+        # BLAS scores (another summation order: within SGEMV_GAP of the sgemv order) pick a superset of every
+        # domain that can be in the exact top K; the superset is then scored in the sgemv order and selected exactly
+        fast = E[rows] @ E.T
         if kk < nd:
-            part = np.argpartition(-sc, kk, axis=1)[:, :kk + 1]
+            Tf = -np.partition(-fast, kk - 1, axis=1)[:, kk - 1]
         else:
-            part = np.broadcast_to(np.arange(nd), (len(rows), nd))
-        ps = np.take_along_axis(sc, part, axis=1)
-        order = np.lexsort((part, -ps), axis=1)
-        top = np.take_along_axis(part, order, axis=1)
-        tops = np.take_along_axis(ps, order, axis=1)
-        cand[rows, :kk] = top[:, :kk]
-        kth[rows] = tops[:, kk - 1]
-        if kk < nd:
-            k1th[rows] = tops[:, kk]
+            Tf = fast.min(axis=1)
+        for j, r in enumerate(rows):
+            sup = np.nonzero(fast[j] >= Tf[j] - SGEMV_GAP)[0]
+            ex = sgemv_scores(E[sup], E[r][None, :])[0]
+            o = np.lexsort((sup, -ex))  # (score desc, index asc)
+            cand[r, :kk] = sup[o[:kk]]
+            kth[r] = ex[o[kk - 1]]
+            if kk < nd:
+                if len(sup) > kk:
+                    k1th[r] = ex[o[kk]]
+                else:  # the (K+1)-th lies more than SGEMV_GAP below: its BLAS score is near enough for a gap test
+                    below = fast[j][fast[j] < Tf[j] - SGEMV_GAP]
+                    k1th[r] = below.max()
     return cand, kth, k1th
 
 

@@ -53,7 +53,19 @@ def match_agreement(idx, sym, err, g, K, cand=None, gap=1e-5, rel=1e-5):
     return exact, equal_fit, near, unexplained
 
 
-#: (idx, sym) agreement with the reference measured for the oracle (same tie order as the HIP kernels) — the
-#: floors the parity tests hold; the remaining mismatches are equal fits (identical tiles) or near-tie candidates.
-MATCH_FLOOR = {("tone", 32): 0.20, ("sweep", 32): 0.998, ("sweep", 64): 0.999, ("noise2048", 64): 1.0,
-               ("noise4096", 64): 1.0, ("speech4096", 64): 0.988, ("ragged", 16): 1.0, ("ragged", 2000): 1.0}
+#: (idx, sym) agreement with the reference measured for the oracle (same scores and tie order as the HIP kernels) —
+#: the floors the parity tests hold; the remaining mismatches are equal fits (identical tiles) or exact-tie
+#: candidate sets.
+MATCH_FLOOR = {("tone", 32): 0.20, ("sweep", 32): 0.999, ("sweep", 64): 1.0, ("noise2048", 64): 1.0,
+               ("noise4096", 64): 1.0, ("speech4096", 64): 0.993, ("ragged", 16): 1.0, ("ragged", 2000): 1.0}
+
+#: scores are bit-identical to the reference's (sgemv order), so candidate sets may differ only where the golden K-th
+#: and (K+1)-th scores are exactly equal (numpy's introselect then chooses among the tied domains)
+EXACT_TIE_GAP = 0.0
+#: the HIP path scores with its OWN embeddings, which are within 1.5e-7 of the reference's (Appendix A rule 2, not
+#: bit-exact), so its scores may differ from the reference's by a few 1e-7 and near-ties at the K-th place may flip:
+#: the GPU tests apply rule 3's 1e-5 gap (given the same embeddings the kernels equal the oracle exactly:
+#: tools/diag/sweep_cands.py)
+GPU_TIE_GAP = 1e-5
+#: (idx, sym) agreement floors for the HIP path (its own embeddings): measured rates, rounded down
+GPU_MATCH_FLOOR = {**MATCH_FLOOR, ("sweep", 32): 0.998, ("sweep", 64): 0.999, ("speech4096", 64): 0.99}

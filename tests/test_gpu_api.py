@@ -97,7 +97,7 @@ def test_cli_outputs_match_reference(tmp_path, case):
     assert np.array_equal(mine[HEADER_SIZE + 32:pool_end], ref[HEADER_SIZE + 32:pool_end])
     rec = mine[pool_end:].copy().view(np.dtype([("idx", "<i4"), ("s", "<f4"), ("o", "<f4"), ("sym", "u1"),
                                                 ("err", "<f4")]))
-    exact, _, _, unexplained = match_agreement(rec["idx"], rec["sym"], rec["err"], g, 32)
+    exact, _, _, unexplained = match_agreement(rec["idx"], rec["sym"], rec["err"], g, 32, gap=1e-5)
     assert not unexplained.any()
     assert np.array_equal(mine[pool_end:].reshape(-1, 17)[exact], ref[pool_end:].reshape(-1, 17)[exact])
     # decompress the reference's .fwav with the CLI defaults (--iter 8 --eps 1e-3)

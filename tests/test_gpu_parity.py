@@ -7,7 +7,7 @@ sets equal except near-ties (golden K-th vs (K+1)-th score gap <= 1e-5) and all-
 import numpy as np
 import pytest
 
-from golden_util import CASES, MATCH_FLOOR, bit_equal, candidate_agreement, load, match_agreement
+from golden_util import CASES, GPU_MATCH_FLOOR, GPU_TIE_GAP, bit_equal, candidate_agreement, load, match_agreement
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -59,10 +59,10 @@ def test_candidates_and_matches(case):
         assert np.array_equal(cand[pruned], gold[pruned])
         zeroq = np.all(g["emb"][:len(cand)] == 0, axis=1) & ~pruned
         assert np.array_equal(cand[zeroq], gold[zeroq]), f"{case} K={K}: Q11 rows differ from the reference"
-        same, bad = candidate_agreement(cand, gold, g[f"kth_{K}"], g[f"k1th_{K}"], None, pruned)
+        same, bad = candidate_agreement(cand, gold, g[f"kth_{K}"], g[f"k1th_{K}"], None, pruned, gap=GPU_TIE_GAP)
         assert not bad.any(), f"{case} K={K}: {bad.sum()} unexplained candidate-set mismatches"
         idx, sym, err = (t.cpu().numpy() for t in (r.idx, r.sym, r.err))
-        exact, equal_fit, near, unexplained = match_agreement(idx, sym, err, g, K)
+        exact, equal_fit, near, unexplained = match_agreement(idx, sym, err, g, K, gap=GPU_TIE_GAP)
         assert not unexplained.any(), f"{case} K={K}: {unexplained.sum()} (idx, sym) mismatches break rule 4"
         for nm, t in (("s", r.s), ("o", r.o), ("err", r.err)):
             assert bit_equal(t.cpu().numpy()[exact], g[f"m_{nm}_{K}"][exact]), f"{case} K={K} {nm}"
@@ -70,7 +70,7 @@ def test_candidates_and_matches(case):
         print(f"{case} K={K}: candidate sets equal {same.mean():.4f}, (idx, sym) equal {rate:.4f}, "
               f"mismatches {(~exact).sum()}: equal fit {(~exact & equal_fit).sum()}, near-tie "
               f"{(~exact & ~equal_fit & near).sum()}")
-        assert rate >= MATCH_FLOOR[(case, K)], f"{case} K={K}: (idx, sym) agreement {rate:.4f}"
+        assert rate >= GPU_MATCH_FLOOR[(case, K)], f"{case} K={K}: (idx, sym) agreement {rate:.4f}"
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -155,8 +155,16 @@ def _cands(sig, tile, K, search, thr=1e-4):
     return r.cand.cpu().numpy().reshape(-1, K), r
 
 
+@pytest.fixture(params=[-1, 0, 1], ids=["mode-auto", "mode-s16", "mode-hl"])
+def first_mode(request):
+    """Run a test under each first-pass mode of the fp16 search (fwav_debug_topk_mode), then restore the default."""
+    call("fwav_debug_topk_mode", request.param)
+    yield request.param
+    call("fwav_debug_topk_mode", -1)
+
+
 @pytest.mark.parametrize("case", CASES)
-def test_f16_prefilter_equals_f32_search(case):
+def test_f16_prefilter_equals_f32_search(case, first_mode):
     """The fp16 pre-filter kernel must select exactly the f32 kernel's candidates (same order)."""
     g = load(case)
     for K in g["p"]["Ks"]:
@@ -171,7 +179,7 @@ def test_f16_prefilter_equals_f32_search(case):
 
 @pytest.mark.parametrize("gen,tile,K", [("noise", 2048, 64), ("speech", 4096, 64), ("noise", 1024, 32),
                                         ("speech", 2048, 17)])
-def test_f16_prefilter_equals_f32_larger(gen, tile, K):
+def test_f16_prefilter_equals_f32_larger(gen, tile, K, first_mode):
     from fwav import synth
     sig = synth.noise(6.0, 44100, seed=11) if gen == "noise" else synth.speech_like(6.0, 44100, seed=5)
     a, _ = _cands(sig, tile, K, "f16")
@@ -187,7 +195,7 @@ def _periodic(n=24000, period=96):
                     ).astype(np.float32)
 
 
-def test_f16_band_overflow_falls_back_to_exact():
+def test_f16_band_overflow_falls_back_to_exact(first_mode):
     """Massive exact ties (≈ 240 equal scores per query) overflow the fp16 band of the key buffer; those queries are
     searched again in exact mode (seeded with the first pass's band limit) — results must stay identical to the
     all-f32 kernel."""
@@ -254,7 +262,7 @@ def test_f16_split_plans_equal_f32(plan):
     assert np.array_equal(p, q)
 
 
-def test_overflow_with_sparse_active_list():
+def test_overflow_with_sparse_active_list(first_mode):
     """max_q bounds the number of listed queries, not their indices: a short active list of large local indices on a
     signal whose fp16 bands overflow must keep the overflow bookkeeping inside the workspace (guard bytes after it
     stay untouched) and return the all-f32 kernel's candidates."""
@@ -268,7 +276,7 @@ def test_overflow_with_sparse_active_list():
     tab = E.embed_tables(rs, sig.device)
     pool = torch.empty(nd * rs, device=sig.device)
     emb = torch.empty(nd * 16, device=sig.device)
-    emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device=sig.device)
+    emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device=sig.device)
     ws = torch.empty(max(size_call("fwav_pool_workspace_size", sig.numel(), tile, rs, step), 16), dtype=torch.uint8,
                      device=sig.device)
     call("fwav_pool_embed", sig.data_ptr(), sig.numel(), tile, rs, step, tab.data_ptr(), pool.data_ptr(),

@@ -3,7 +3,7 @@ tests/golden/make_golden.py from /root/reference/fractal.py).  Bars: SURVEY.md A
 import numpy as np
 import pytest
 
-from golden_util import CASES, MATCH_FLOOR, bit_equal, candidate_agreement, load, match_agreement
+from golden_util import CASES, EXACT_TIE_GAP, MATCH_FLOOR, bit_equal, candidate_agreement, load, match_agreement
 from oracle import fractal_oracle as O
 
 
@@ -37,7 +37,7 @@ def test_candidates_near_tie_rule(case):
         gold = g[f"cand_{K}"]
         assert np.array_equal(pruned, gold[:, 0] < 0)
         cand, _, _ = O.topk_candidates(g["emb"], len(gold), K, pruned)
-        _, bad = candidate_agreement(cand, gold, g[f"kth_{K}"], g[f"k1th_{K}"], None, pruned)
+        _, bad = candidate_agreement(cand, gold, g[f"kth_{K}"], g[f"k1th_{K}"], None, pruned, gap=EXACT_TIE_GAP)
         assert not bad.any()
         zeroq = np.all(g["emb"][:len(gold)] == 0, axis=1) & ~pruned
         assert np.array_equal(cand[zeroq], gold[zeroq])  # quirk Q11: the reference's own tie order
@@ -53,7 +53,7 @@ def test_end_to_end_rule4(case):
     for K in p["Ks"]:
         cand, _, _ = O.topk_candidates(g["emb"], len(pruned), K, pruned)
         idx, s, o, sym, err = O.affine(g["ranges"], cand, g["pool"])
-        exact, _, _, unexplained = match_agreement(idx, sym, err, g, K)
+        exact, _, _, unexplained = match_agreement(idx, sym, err, g, K, gap=EXACT_TIE_GAP)
         assert not unexplained.any()
         assert exact.mean() >= MATCH_FLOOR[(case, K)]
 

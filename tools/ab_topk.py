@@ -29,7 +29,7 @@ r = engine.compress_device(sig, tile, 64, keep_intermediates=True)
 torch.cuda.synchronize()
 nd, nr = r.n_domains, r.n_ranges
 rs, step = engine.geometry(tile)
-emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 from fwav._lib import call  # noqa: E402
 tab = engine.embed_tables(rs, torch.device("cuda"))
 pool = torch.empty(nd * rs, device="cuda")

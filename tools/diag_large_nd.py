@@ -27,7 +27,7 @@ nd = res.n_domains
 print("nd", nd, "nr", nr, flush=True)
 emb = res.emb.view(-1, 16)
 # rebuild emb16 through the public entry point to inspect it
-emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 tab = engine.embed_tables(rs, torch.device("cuda"))
 from fwav._lib import size_call  # noqa: E402
 wsn = size_call("fwav_pool_workspace_size", n, tile, rs, 2)

@@ -31,7 +31,7 @@ step = r.domain_step if hasattr(r, "domain_step") else None
 from oracle import fractal_oracle as O  # noqa: E402  (tools: geometry only)
 rs2, step = O.geometry(p["tile"])[:2]
 assert rs2 == rs
-emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 tab = engine.embed_tables(rs, torch.device("cuda"))
 pool = torch.empty(nd * rs, device="cuda")
 emb2 = torch.empty(nd * 16, device="cuda")

@@ -31,7 +31,7 @@ torch.cuda.synchronize()
 ref = r.cand.cpu().numpy().reshape(-1, K)
 nd, nr = r.n_domains, r.n_ranges
 rs, step = O.geometry(p["tile"])[:2]
-emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 tab = engine.embed_tables(rs, torch.device("cuda"))
 pool = torch.empty(nd * rs, device="cuda")
 emb = torch.empty(nd * 16, device="cuda")

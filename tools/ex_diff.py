@@ -29,7 +29,7 @@ torch.cuda.synchronize()
 nd, nr = r.n_domains, r.n_ranges
 rs, step = engine.geometry(tile)
 st = torch.cuda.current_stream().cuda_stream
-emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 tab = engine.embed_tables(rs, torch.device("cuda"))
 pool = torch.empty(nd * rs, device="cuda")
 emb = torch.empty(nd * 16, device="cuda")

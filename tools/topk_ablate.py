@@ -18,7 +18,7 @@ sig = torch.from_numpy(synth.noise(secs, 44100)).cuda()
 r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
 torch.cuda.synchronize()
 nd, nr = r.n_domains, r.n_ranges
-emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 # rebuild emb16 through the pool+embed entry point
 r2 = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
 st = torch.cuda.current_stream().cuda_stream

@@ -21,7 +21,7 @@ sig = torch.from_numpy(synth.noise(60.0, 44100)).cuda()
 r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
 torch.cuda.synchronize()
 nd, nr = r.n_domains, r.n_ranges
-emb16 = torch.empty(((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 tab = engine.embed_tables(8, torch.device("cuda"))
 pool = torch.empty(nd * 8, device="cuda")
 emb = torch.empty(nd * 16, device="cuda")
