@@ -398,13 +398,14 @@ constexpr int kMaxPieces = 8;        // a split block's table pieces (merge: P·
 // half block on a CU of its own runs its waves faster than a full block.
 struct TopkPlan {
   int64_t nb, F, R;
-  int P;
+  int P, qb;
   bool halves;
   __host__ __device__ int64_t items() const { return F + R * P; }
 };
-__host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P) {
+__host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, int qb) {
   TopkPlan pl;
-  pl.nb = cdiv(n_queries > 0 ? n_queries : 0, k16QB);
+  pl.qb = qb;
+  pl.nb = cdiv(n_queries > 0 ? n_queries : 0, qb);
   pl.halves = P < 0;
   pl.P = pl.halves ? 2 : (P < 1 ? 1 : (P > kMaxPieces ? kMaxPieces : P));
   pl.R = pl.P == 1 ? 0 : (pl.nb < rt ? pl.nb : (int64_t)rt);
@@ -417,11 +418,12 @@ __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P) 
 #ifndef FWAV_TOPK_INTERLEAVE
 #define FWAV_TOPK_INTERLEAVE 1
 #endif
-__host__ __device__ inline int64_t slot_query(int64_t block, int ql, int64_t nb) {
+__host__ __device__ inline int64_t slot_query(int64_t block, int ql, int64_t nb, int qb) {
 #if FWAV_TOPK_INTERLEAVE
+  (void)qb;
   return ((int64_t)(ql >> 5) * nb + block) * 32 + (ql & 31);
 #else
-  return block * k16QB + ql;
+  return block * qb + ql;
 #endif
 }
 // item → (block, table piece, table pieces, query half: −1 = the whole block)
@@ -1061,7 +1063,8 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
   Topk16SmemT<NG, STATS>& sm = lds_all.sm;
 
   const int n_active = *n_active_p;
-  const TopkPlan plan = make_plan(n_active, plan_rt, plan_p);
+  constexpr int QB = 32 * NG;  // queries per block
+  const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
   int64_t block;
   int piece, npieces, qhalf;
   plan_item(plan, blockIdx.x, block, piece, npieces, qhalf);
@@ -1098,7 +1101,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     const int ql = (wave * QS + s) * 32 + col;
-    const int64_t qi = slot_query(block, qslot0 + ql, plan.nb);
+    const int64_t qi = slot_query(block, qslot0 + ql, plan.nb, QB);
     const int32_t q = qi < n_active ? active[qi] : -1;
     const int64_t qrow = (int64_t)(q < 0 ? 0 : q) + q_offset;
     b[s] = *reinterpret_cast<const half8*>(emb16 + (((qrow >> 8) * 2 + h) * 256 + (qrow & 255)) * 8);
@@ -1132,14 +1135,14 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
 #ifdef FWAV_TOPK_EXTSEED
       // experiment builds: a host-computed lower bound per active query (gstats reinterpreted as float[n_active])
       if (upd[s] && gstats != nullptr)
-        thf[s] = fmaxf(thf[s], reinterpret_cast<const float*>(gstats)[slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb)]);
+        thf[s] = fmaxf(thf[s], reinterpret_cast<const float*>(gstats)[slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb, QB)]);
 #endif
 #ifdef FWAV_TOPK_DEBUG
       if (upd[s] && sm.qrow[(wave * QS + s) * 32 + col] < (1 << 19))
         g_fwav_dbg[sm.qrow[(wave * QS + s) * 32 + col] + (h << 19)] = __float_as_uint(seed);
 #endif
       if (STATS && (dbg & 32768) && gstats != nullptr && h == 0 && upd[s])  // diagnostics: the seeds
-        gstats[16 + slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb)] = __float_as_uint(seed);
+        gstats[16 + slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb, QB)] = __float_as_uint(seed);
     }
   }
   if (seeds_in != nullptr) {
@@ -1362,7 +1365,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
 
   for (int l = 0; l < 32 * QS; ++l) {
     const int qs = wave * QS * 32 + l;
-    const int64_t qq = slot_query(block, qslot0 + qs, plan.nb);
+    const int64_t qq = slot_query(block, qslot0 + qs, plan.nb, QB);
     if (qq >= n_active) continue;
     const int32_t qid = active[qq];
     uint64_t* kq = gkeys + (size_t)qs * C;
@@ -1397,7 +1400,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
 // Merge the pieces of split blocks: per query, the P sorted exact top-K key lists of its block's pieces → the
 // top K of their union (the top K of a union is the top K of the parts' top Ks), ties by index as everywhere.
 // One wave per query; a query flagged by any piece goes to the exact-mode relaunch list once, with the largest seed.
-template <int C>
+template <int C, int QB>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
                                                       const int32_t* __restrict__ n_active_p, int plan_rt, int plan_p,
@@ -1405,13 +1408,13 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
                                                       int32_t* __restrict__ n_ovf) {
   constexpr int E = kMaxPieces;  // ≤ 8 pieces × K ≤ 64 keys = 512 = 8 per lane
   const int n_active = *n_active_p;
-  const TopkPlan plan = make_plan(n_active, plan_rt, plan_p);
+  const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // split-block query index
-  if (plan.R == 0 || plan.halves || w >= plan.R * k16QB) return;
+  if (plan.R == 0 || plan.halves || w >= plan.R * QB) return;
   const int lane = threadIdx.x & 63;
-  const int64_t block = plan.F + w / k16QB;
-  const int ql = (int)(w % k16QB);
-  const int64_t qq = slot_query(block, ql, plan.nb);
+  const int64_t block = plan.F + w / QB;
+  const int ql = (int)(w % QB);
+  const int64_t qq = slot_query(block, ql, plan.nb, QB);
   if (qq >= n_active) return;
   const int P = plan.P;
   uint64_t v[E];
@@ -1424,7 +1427,7 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
     v[j] = 0ull;
     if (p < P) {
       const int64_t item = plan.F + (block - plan.F) * P + p;
-      const uint64_t* kq = gkeys_all + ((size_t)item * k16QB + ql) * C;
+      const uint64_t* kq = gkeys_all + ((size_t)item * QB + ql) * C;
       v[j] = kq[r];
       if (r == 0) seed = max(seed, (uint32_t)kq[C - 1]);
     }
@@ -1456,19 +1459,37 @@ static int current_device() {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
   return dev;
 }
-static void topk_device_slots(int& cus, int& per_cu) {
-  static int cs[kMaxDev] = {0}, ws[kMaxDev] = {0};
+// First-pass geometry.  Tables of more than kWideMinDomains domains (an fp16 table of > 128 MB, on its way past the
+// 256 MB Infinity Cache) take the wide workgroup: kWideW = 16 waves × 32 queries, one workgroup per CU (its LDS holds
+// 2 × 8 chunk slots, one barrier per 8 chunks), so a CU streams the table once for 512 queries where the base
+// geometry streams it twice for 2 × 256.  Same-box A/B on a cfg4 shard (86.4 M domains × 337,500 queries, identical
+// outputs): base 973.8 ms, W = 16 / G = 4 963.3, W = 16 / G = 8 944.0, QS = 2 (233 VGPRs: 2 waves per SIMD) 1,088;
+// cfg2 (1.3 M domains, MALL-resident table): base 20.7 ms, wide 21.7; cfg3 (6.6 M, a 212 MB table): base 187.6,
+// wide 193.4; cfg4 shard again: base 962.2, wide 945.6 — so the wide geometry is used only where the table (32 B per
+// domain) no longer fits the Infinity Cache.  Relaunches on overflow lists keep the base geometry (few queries).
+#ifndef FWAV_TOPK_WIDE_MIN
+#define FWAV_TOPK_WIDE_MIN (int64_t(1) << 23)
+#endif
+constexpr int kWideW = 16, kWideG = 8;
+constexpr int kWideQB = 32 * kWideW;
+static int g_wide = -1;  // fwav_debug_topk_geometry (tests): force base / wide
+static bool wide_geometry(int64_t nd) { return g_wide >= 0 ? g_wide != 0 : nd > (int64_t)FWAV_TOPK_WIDE_MIN; }
+
+static void topk_device_slots(bool wide, int& cus, int& per_cu) {
+  static int cs[2][kMaxDev] = {{0}}, ws[2][kMaxDev] = {{0}};
   const int dev = current_device();
-  int& c = cs[dev];
-  int& w = ws[dev];
+  int& c = cs[wide][dev];
+  int& w = ws[wide][dev];
   if (c == 0) {
-    if (!(
-          hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeS16>, 64 * k16Waves, 0) ==
-              hipSuccess &&
+    const hipError_t occ =
+        wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeHL, kWideW, kWideG>,
+                                                            64 * kWideW, 0)
+             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeS16>, 64 * k16Waves,
+                                                            0);
+    if (!(hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && occ == hipSuccess &&
           c > 0 && w > 0)) {
-      c = 256;  // MI355X: 256 CUs × 2 workgroups
-      w = 2;
+      c = 256;  // MI355X: 256 CUs × 2 base (1 wide) workgroups
+      w = wide ? 1 : 2;
     }
   }
   cus = c;
@@ -1481,15 +1502,15 @@ static void topk_device_slots(int& cus, int& per_cu) {
 // fill in beside the lone workgroups (cfg2 A/B: 24.9 → 22.6 ms; splitting more blocks costs more than it saves,
 // since every piece restarts the rising limit: 268 blocks in 2 pieces 24.2 ms, 512 in 2 25.3 ms).  Few blocks
 // (at most half the slots) are each split into up to 8 pieces so that the table passes use the idle CUs.
-static void host_plan_for(int64_t max_q, int64_t nd, int& rt, int& P) {
+static void host_plan_for(int64_t max_q, int64_t nd, bool wide, int& rt, int& P) {
   if (g_plan_rt >= 0) {  // diagnostic override
     rt = g_plan_rt;
     P = g_plan_p;
   } else {
     int cus, per_cu;
-    topk_device_slots(cus, per_cu);
+    topk_device_slots(wide, cus, per_cu);
     const int64_t slots = (int64_t)cus * per_cu;
-    const int64_t nb = cdiv(max_q > 0 ? max_q : 1, k16QB);
+    const int64_t nb = cdiv(max_q > 0 ? max_q : 1, wide ? kWideQB : k16QB);
     rt = 0;
     P = 1;
     if (2 * nb <= slots) {
@@ -1507,11 +1528,19 @@ static void host_plan_for(int64_t max_q, int64_t nd, int& rt, int& P) {
   const int64_t pmax = cdiv(nd, kChunk) / 16;
   if (P > pmax) P = (int)(pmax > 1 ? pmax : 1);
 }
+// Key-buffer bytes: enough for the first pass in either geometry (a diagnostic override may switch it between the
+// size query and the launch) and for the relaunches' base plan.
 static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
-  int rt, P;
-  host_plan_for(max_q, nd, rt, P);
-  const TopkPlan pl = make_plan(max_q > 0 ? max_q : 1, rt, P);
-  return (size_t)pl.items() * k16QB * k16Cap * sizeof(uint64_t);
+  const int64_t q = max_q > 0 ? max_q : 1;
+  size_t items_q = (size_t)make_plan(q, 0, 1, k16QB).items() * k16QB;
+  for (int wide = 0; wide < 2; ++wide) {
+    int rt, P;
+    host_plan_for(q, nd, wide != 0, rt, P);
+    const int qb = wide ? kWideQB : k16QB;
+    const size_t n = (size_t)make_plan(q, rt, P, qb).items() * qb;
+    items_q = n > items_q ? n : items_q;
+  }
+  return items_q * k16Cap * sizeof(uint64_t);
 }
 
 template <int C>
@@ -1544,14 +1573,19 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     (void)hipMemsetAsync(n_ovf2, 0, sizeof(int32_t), st);
     // Geometry: k16Waves waves × k16Sets query sets of 32 per workgroup.  Measured at cfg2 (W, QS=1): W = 8
     // 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms — an even 4 waves per SIMD beats a fuller last round of workgroups.
-    int rt, P;
-    host_plan_for(max_q, nd, rt, P);
-    const TopkPlan pl = make_plan(max_q, rt, P);
     const bool stats_first = (stats != nullptr && !(dbg & (1 << 17))) || (dbg & 65535) != 0;
+    // counter (STATS) builds of the first pass exist in the base geometry only
+    const bool wide = !stats_first && wide_geometry(nd);
+    int rt, P;
+    host_plan_for(max_q, nd, wide, rt, P);
+    const TopkPlan pl = make_plan(max_q, rt, P, wide ? kWideQB : k16QB);
     const int mode1 = first_mode(nd);
 #define FWAV_FIRST(MODE_, STATS_, DBG_, ST_)                                                                    \
   k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, 0, st>>>(                                 \
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, nullptr, 0.0f, rt, P, DBG_, ST_)
+#define FWAV_FIRST_WIDE(MODE_)                                                                                   \
+  k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG><<<pl.items(), 64 * kWideW, 0, st>>>(                    \
+      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, nullptr, 0.0f, rt, P, 0, nullptr)
 #ifdef FWAV_TOPK_EXTSEED
     if (stats != nullptr && dbg == 0) {
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
@@ -1560,18 +1594,26 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     if (stats_first) {
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, true, dbg & 65535, stats);
       else FWAV_FIRST(kModeS16, true, dbg & 65535, stats);
+    } else if (wide) {
+      if (mode1 == kModeHL) FWAV_FIRST_WIDE(kModeHL); else FWAV_FIRST_WIDE(kModeS16);
     } else {
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, nullptr); else FWAV_FIRST(kModeS16, false, 0, nullptr);
     }
 #undef FWAV_FIRST
-    if (pl.R > 0)
-      k_merge_pieces<k16Cap><<<cdiv(pl.R * k16QB, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, ovf1,
-                                                                    n_ovf1);
+#undef FWAV_FIRST_WIDE
+    if (pl.R > 0) {
+      if (wide)
+        k_merge_pieces<k16Cap, kWideQB><<<cdiv(pl.R * kWideQB, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K,
+                                                                               cand, ovf1, n_ovf1);
+      else
+        k_merge_pieces<k16Cap, k16QB><<<cdiv(pl.R * k16QB, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand,
+                                                                            ovf1, n_ovf1);
+    }
     // Queries whose band overflowed the buffer (large groups of equal or nearly equal scores) are searched again by
     // the same kernel in a narrower mode, on the device-side overflow list (no host sync; a relaunch exits at once
     // when its list is empty): after an S16 first pass the HL mode, then the exact mode for what still overflows;
     // after an HL first pass the exact mode, whose compactions keep exactly the top K, so nothing overflows.
-    const TopkPlan pl_re = make_plan(max_q, 0, 1);
+    const TopkPlan pl_re = make_plan(max_q, 0, 1, k16QB);
     const int32_t* ex_in = ovf1;
     const int32_t* ex_n = n_ovf1;
     const uint32_t* ex_seeds = seeds1;
@@ -1673,6 +1715,14 @@ int fwav_debug_dump(void* host, size_t bytes, unsigned* n_events) {
 int fwav_debug_topk_mode(int mode) {
   FWAV_CHECK_ARG(mode >= -1 && mode <= 1, FWAV_ERR_ARG, "fwav_debug_topk_mode: mode outside [-1, 1]");
   g_first_mode = mode;
+  return FWAV_OK;
+}
+
+// Diagnostic override of the first pass's geometry: 0 = base (8 waves, 256 queries per workgroup), 1 = wide (16
+// waves, 512 queries, one workgroup per CU), −1 = by table size (default).  Both return the same candidates.
+int fwav_debug_topk_geometry(int wide) {
+  FWAV_CHECK_ARG(wide >= -1 && wide <= 1, FWAV_ERR_ARG, "fwav_debug_topk_geometry: outside [-1, 1]");
+  g_wide = wide;
   return FWAV_OK;
 }
 

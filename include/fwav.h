@@ -108,6 +108,11 @@ int fwav_debug_topk_plan(int rt, int pieces);
  * hi/lo band, then exact keys), 1 = hi/lo band (then exact keys), −1 = by table size (the default: hi/lo above 4 Mi
  * domains).  Every mode returns the same candidates. */
 int fwav_debug_topk_mode(int mode);
+/* Diagnostic override of the fp16 search's first-pass geometry: 0 = 8 waves × 32 queries per workgroup, 1 = 16 waves
+ * × 32 queries, one workgroup per CU (the table streamed once per 512 queries), −1 = by table size (the default: wide
+ * above 8 Mi domains, where the table outgrows the Infinity Cache).  Both return the same candidates.  Re-query
+ * fwav_sim_topk_workspace_size afterwards. */
+int fwav_debug_topk_geometry(int wide);
 
 /* ------------------------------------------------------------------- batched affine solve
  * Replaces _flush_gpu_batch / _process_gpu_batch (fractal.py:852-870, 757-850): per range, over the K

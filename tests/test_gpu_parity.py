@@ -155,12 +155,17 @@ def _cands(sig, tile, K, search, thr=1e-4):
     return r.cand.cpu().numpy().reshape(-1, K), r
 
 
-@pytest.fixture(params=[-1, 0, 1], ids=["mode-auto", "mode-s16", "mode-hl"])
+@pytest.fixture(params=[(-1, -1), (0, 0), (1, 0), (0, 1), (1, 1)],
+                ids=["auto", "s16-base", "hl-base", "s16-wide", "hl-wide"])
 def first_mode(request):
-    """Run a test under each first-pass mode of the fp16 search (fwav_debug_topk_mode), then restore the default."""
-    call("fwav_debug_topk_mode", request.param)
-    yield request.param
+    """Run a test under each first-pass mode (fwav_debug_topk_mode) and workgroup geometry (fwav_debug_topk_geometry)
+    of the fp16 search, then restore the defaults."""
+    mode, wide = request.param
+    call("fwav_debug_topk_mode", mode)
+    call("fwav_debug_topk_geometry", wide)
+    yield mode
     call("fwav_debug_topk_mode", -1)
+    call("fwav_debug_topk_geometry", -1)
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -243,8 +248,9 @@ def test_large_k_vs_oracle(K):
     assert not bad.any(), f"K={K}: {bad.sum()} unexplained mismatches"
 
 
+@pytest.mark.parametrize("wide", [0, 1], ids=["base", "wide"])
 @pytest.mark.parametrize("plan", [(0, 1), (1 << 20, 2), (1 << 20, 5), (1 << 20, 8), (10, 3), (1 << 20, -1), (7, -1)])
-def test_f16_split_plans_equal_f32(plan):
+def test_f16_split_plans_equal_f32(plan, wide):
     """Work plans that split query blocks into table pieces (merged by k_merge_pieces) or into query halves return
     exactly the unsplit search's candidates: whole, all blocks in 2/5/8 pieces, only the last 10 blocks in 3, and all /
     the last 7 blocks as two half-blocks (4 waves each; the other waves exit at once)."""
@@ -252,11 +258,13 @@ def test_f16_split_plans_equal_f32(plan):
     sig = synth.noise(6.0, 44100, seed=11)
     b, _ = _cands(sig, 2048, 64, "f32")
     call("fwav_debug_topk_plan", *plan)
+    call("fwav_debug_topk_geometry", wide)
     try:
         a, _ = _cands(sig, 2048, 64, "f16")
         p, _ = _cands(_periodic(), 1024, 32, "f16")  # band overflow inside pieces → exact-mode relaunch after the merge
     finally:
         call("fwav_debug_topk_plan", -1, 1)
+        call("fwav_debug_topk_geometry", -1)
     assert np.array_equal(a, b)
     q, _ = _cands(_periodic(), 1024, 32, "f32")
     assert np.array_equal(p, q)

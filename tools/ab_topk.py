@@ -25,7 +25,9 @@ cfg = os.environ.get("AB_CFG", "cfg2")  # cfg3: the speech-like 10 min case (its
 sig_h, _, _ = synth.make_config_signal(cfg)
 tile = synth.CONFIGS[cfg]["tile"]
 sig = torch.from_numpy(sig_h).cuda()
-r = engine.compress_device(sig, tile, 64, keep_intermediates=True)
+# cfg4: only the geometry is needed from the engine run (the harness builds its own table below; searching all
+# 21.6 M ranges would take a minute)
+r = engine.compress_device(sig, tile, 64, keep_intermediates=True, shard=(0, 256) if cfg == "cfg4" else None)
 torch.cuda.synchronize()
 nd, nr = r.n_domains, r.n_ranges
 rs, step = engine.geometry(tile)
@@ -39,8 +41,8 @@ ws = torch.empty(max(wsp, 16), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 call("fwav_pool_embed", sig.data_ptr(), sig.numel(), tile, rs, step, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
      emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
-if cfg == "cfg2":
-    nq = int(os.environ.get("AB_NQ", nr))  # active queries (default: all ranges)
+if cfg in ("cfg2", "cfg4"):  # noise: every range active; cfg4 default = one rank's 1/64 of the ranges
+    nq = int(os.environ.get("AB_NQ", nr if cfg == "cfg2" else 337_500))  # active queries (default: all ranges)
     active = torch.arange(nq, dtype=torch.int32, device="cuda")
 else:  # the engine's own pruned active list
     nq = int(r.n_active.item())
