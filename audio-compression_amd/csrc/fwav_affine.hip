@@ -266,6 +266,9 @@ __device__ __forceinline__ void affine_one(const float (&R)[RS], int64_t r, int3
 #define FWAV_AFF_BATCH 4
 #endif
 constexpr int kAffBatch = FWAV_AFF_BATCH;  // ranges per wave in k_affine_batch
+#ifndef FWAV_AFF_ABL
+#define FWAV_AFF_ABL 0
+#endif
 #ifndef FWAV_AFF_XCD
 #define FWAV_AFF_XCD 1
 #endif
@@ -301,6 +304,16 @@ __global__ __launch_bounds__(64 * kAffWaves) void k_affine_batch(const float* __
   float D[kAffBatch][RS];
 #pragma unroll
   for (int j = 0; j < kAffBatch; ++j) gather_row<RS>(pool, c[j], D[j]);
+#if FWAV_AFF_ABL
+  // ablation build (tools/affine_probe.py): the same loads, no solve — the memory side's time alone
+  float acc = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kAffBatch; ++j)
+#pragma unroll
+    for (int i = 0; i < RS; ++i) acc += D[j][i];
+  if (acc == 1.2345f) out_err[r0] = acc;
+  return;
+#endif
   // range rows: wave-uniform and read-only → constant address space → scalar loads
   const __attribute__((address_space(4))) float* rg = (const __attribute__((address_space(4))) float*)ranges;
 #pragma unroll

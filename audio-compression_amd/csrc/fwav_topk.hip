@@ -490,6 +490,7 @@ struct Topk16SmemT {
   int cnt1[32 * NG];  // ... and at the back (its h = 1 lane's)
   int ovf[32 * NG];  // band overflowed the buffer (f2key of its band limit, else 0): recompute in exact mode
   int64_t qrow[32 * NG];
+  int32_t qpos[32 * NG];  // position of the slot's query in the active list (index of its shared band limit)
   uint32_t fired[NG][kFifo];                       // deferred work: ring of fired chunk entries
   unsigned long long wstat[STATS ? NG : 1][kStats];  // STATS builds only (one row per wave)
 };
@@ -567,8 +568,8 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0,
   }
 }
 
-// Final pass of query ql: rescore its two-ended buffer (sm.cnt entries at the front, sm.cnt1 at the back) in exact
-// f32 (sgemv16), sort, emit the top K (to `out`, or for a piece back into kq).  Whole wave.  Every per-query buffer and
+// Final pass of query ql (a whole-table item): rescore its two-ended buffer (sm.cnt entries at the front, sm.cnt1 at
+// the back) in exact f32 (sgemv16), sort, emit the top K to `out`.  Whole wave.  Every per-query buffer and
 // counter is owned by one wave, so no cross-wave fences are needed; the wave's own appended stores are drained
 // once (vmcnt(0)), then all key loads and all row loads are issued together (two memory round trips in total).
 template <int C, class SM>
@@ -618,18 +619,64 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
   }
   wave_sort_desc<E>(v);
   // Emit straight from registers (never read back what was just stored: a load issued right behind the stores
-  // of the same addresses can return the old contents).  A whole-table item writes the K candidate indices,
-  // −1-padded; a piece leaves its sorted exact top K in the buffer, 0-padded, for k_merge_pieces.
+  // of the same addresses can return the old contents): the K candidate indices, −1-padded.
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
-    if (e < K) {
-      if (out != nullptr)
-        out[e] = e < n ? key_idx(v[j]) : -1;
-      else
-        kq[e] = e < n ? v[j] : 0ull;
-    }
+    if (e < K) out[e] = e < n ? key_idx(v[j]) : -1;
   }
+}
+
+// End of a table piece (split block): no rescoring and no sort here — the piece keeps the entries of its band whose
+// key beats the query's shared limit (Lk, the f2key of the largest band limit any piece of the query has published;
+// every exact top-K member's key is above it), written densely at the front of its buffer, and a header in the last
+// slot: (overflow key << 32) | count.  k_merge_pieces rescores and sorts the union of the pieces' bands once per
+// query.  A band that would not leave 64 slots is flagged as overflowed (the query goes to the exact-mode relaunch).
+template <int C, bool HL, class SM>
+__device__ __forceinline__ void piece_band(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
+                                           uint32_t* __restrict__ share_q) {
+  constexpr int E = C / 64;
+  const int lane = threadIdx.x & 63;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int n0 = sm.cnt[ql];
+  const int n = min(n0 + sm.cnt1[ql], C);
+  uint64_t v[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    v[j] = e < n ? ld_key(kq + two_end_slot<C>(e, n0)) : 0ull;
+  }
+  // the piece's own limit now (a last compaction's select over its whole buffer), published before the filter so
+  // that the pieces still streaming and k_merge_pieces see it
+  uint32_t Lk = 0u;
+  if (n >= K) {
+    uint32_t T = 0;
+    for (int bit = 31; bit >= (HL ? 0 : 12); --bit) {
+      const uint32_t Tc = T | (1u << bit);
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < E; ++j) c += __popcll(__ballot((uint32_t)(v[j] >> 32) >= Tc));
+      if (c >= K) T = Tc;
+    }
+    Lk = f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta);
+    if (lane == 0) atomicMax(share_q, Lk);
+  }
+  Lk = max(Lk, __hip_atomic_load(share_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  int m = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const bool keep = v[j] != 0ull && (uint32_t)(v[j] >> 32) > Lk;
+    const uint64_t bm = __ballot(keep);
+    const int pos = m + __popcll(bm & ((1ull << lane) - 1ull));
+    if (keep && pos < C - 64) kq[pos] = v[j];
+    m += __popcll(bm);
+  }
+  uint32_t ovf = (uint32_t)sm.ovf[ql];
+  if (m > C - 64) {
+    m = C - 64;
+    if (ovf == 0u) ovf = Lk != 0u ? Lk : 1u;  // any nonzero flag; the limit (if any) is a valid relaunch seed
+  }
+  if (lane == 0) kq[C - 1] = ((uint64_t)ovf << 32) | (uint32_t)m;
 }
 
 // Integer filter threshold for the fold-max test: (int)x > thi ⟺ x > thf for non-NaN x when thf >= 0;
@@ -691,7 +738,8 @@ template <int C, bool STATS, class SM, int MODE>
 __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int& qcnt, int& kept, int64_t dt, int64_t nd,
                                              uint64_t* __restrict__ gkeys, SM& sm, int qg, int K, int upd,
                                              unsigned long long* stats, const float* __restrict__ emb = nullptr,
-                                             const float* qv = nullptr, uint64_t* kthp = nullptr) {
+                                             const float* qv = nullptr, uint64_t* kthp = nullptr,
+                                             uint32_t* __restrict__ share = nullptr) {
   constexpr bool EX = MODE == kModeEX;
   const int lane = threadIdx.x & 63;
   const int col = lane & 31;
@@ -799,6 +847,8 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
       qcnt = h ? 0 : m;  // the kept band is written densely at the front
       kept = m;
       if (upd) thf = fmaxf(thf, lim);  // the seed may be above a buffer's own limit
+      // a table piece publishes its limit to the query's other pieces (shared_limit below)
+      if (share != nullptr && h == 0 && lim > -INFINITY) atomicMax(share + sm.qpos[qg * 32 + l], f2key(lim));
       // a query whose band overflowed is searched again in exact mode: stop appending for it here
       if (!EX && sm.ovf[qg * 32 + l]) thf = INFINITY;
       if (EX) *kthp = kth_l;
@@ -852,7 +902,7 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
                                                int& kept, ReplayCursor& cur, int tail, int64_t nd, uint64_t* __restrict__ gkeys,
                                                SM& sm, int qg, int K, int upd, unsigned long long* stats,
                                                const float* __restrict__ emb = nullptr, const float* qv = nullptr,
-                                               uint64_t* kthp = nullptr) {
+                                               uint64_t* kthp = nullptr, uint32_t* __restrict__ share = nullptr) {
   constexpr bool HL = MODE == kModeHL;
   const int lane = threadIdx.x & 63;
   const int col = lane & 31;
@@ -890,7 +940,7 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl[u], b, acc, 0, 0, 0);
       }
       thf = append_tile<C, STATS, SM, MODE>(acc, thf, qcnt, kept, ct[u], nd, gkeys, sm, qg, K, upd, stats, emb, qv,
-                                          kthp);
+                                          kthp, share);
     }
     if (ct[kReplayBatch - 1] < 0) break;
   }
@@ -1040,6 +1090,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
                                                                 uint64_t* __restrict__ gkeys_all,
                                                                 int32_t* __restrict__ ovf_list,
                                                                 int32_t* __restrict__ n_ovf,
+                                                                uint32_t* __restrict__ share_lim,
                                                                 const uint32_t* __restrict__ seeds_in,
                                                                 float seed_shift, int plan_rt,
                                                                 int plan_p, int dbg, unsigned long long* gstats) {
@@ -1098,6 +1149,11 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
   const _Float16* emb16lo = emb16 + n16;
   uint64_t kth[QS];           // EX: the query's current K-th exact key (0 until K entries)
   float inseed[QS];           // relaunch: the previous pass's band limit at overflow, in this mode's scale
+  int32_t qpos[QS];           // the slot's query position in the active list
+  // Table pieces of one query block share their band limits: a piece's compaction limit is a valid lower bound for
+  // the whole query (K domains of its own chunk range beat it), so every piece filters with the largest limit any
+  // piece has found (atomicMax on the f2key, read back at window ends) instead of restarting its own rise.
+  uint32_t* share = (npieces > 1 && !EX) ? share_lim : nullptr;
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     const int ql = (wave * QS + s) * 32 + col;
@@ -1108,9 +1164,11 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
     bl[s] = *reinterpret_cast<const half8*>(emb16lo + (((qrow >> 8) * 2 + h) * 256 + (qrow & 255)) * 8);
     upd[s] = (q >= 0 && !(dbg & 1)) ? 1 : 0;
     thf[s] = upd[s] ? -INFINITY : INFINITY;  // slots past n_active never take appends
+    qpos[s] = (int32_t)(qi < n_active ? qi : 0);
     if (h == 0) {
       sm.ovf[ql] = 0;
       sm.qrow[ql] = qrow;
+      sm.qpos[ql] = qpos[s];
     }
     kth[s] = 0ull;
     // relaunch: active = the previous pass's overflow list, whose position qi holds this query's seed (that pass's
@@ -1279,7 +1337,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
         for (int s = 0; s < QS; ++s) {
           if (nfired[s] > cur[s].head || cur[s].rem != 0u)
             thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s], qcnt[s], kept[s], cur[s],
-                                             nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s]);
+                                             nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s], share);
         }
         if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
         __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -1339,12 +1397,19 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
     const unsigned long long t_c = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(9, t_c - t_b1);
     if (window_end) {
+      if (share != nullptr) {  // the largest limit the query's pieces have published
+#pragma unroll
+        for (int s = 0; s < QS; ++s) {
+          const uint32_t v = __hip_atomic_load(share + qpos[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (upd[s] && v != 0u) thf[s] = fmaxf(thf[s], key2f(v));
+        }
+      }
       // each wave replays its own fired chunks (compacting inline when a buffer fills)
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
         if (nfired[s] > cur[s].head || cur[s].rem != 0u)
           thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s], qcnt[s], kept[s], cur[s],
-                                           nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s]);
+                                           nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s], share);
       }
       if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
       // retire the replay's loads and stores here, visibly to hipcc's wait bookkeeping (vmcnt(0) expcnt(7)
@@ -1370,18 +1435,17 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
     const int32_t qid = active[qq];
     uint64_t* kq = gkeys + (size_t)qs * C;
     if (lane == 0) FWAV_TRACE(sm.qrow[qs], 3u, (uint32_t)sm.cnt[qs], (uint32_t)sm.ovf[qs], (uint32_t)sm.cnt1[qs]);
-    // exact f32 rescoring of the kept band + sort; a piece keeps its top K in the buffer, the overflow flag in the
-    // last entry (k_merge_pieces combines the block's pieces)
-    compact16<C>(kq, sm, qs, K, emb, npieces == 1 ? cand + (int64_t)qid * K : nullptr);
+    if (npieces > 1) {  // a table piece hands its filtered band to k_merge_pieces
+      piece_band<C, HL>(kq, sm, qs, K, share_lim + qq);
+      continue;
+    }
+    // exact f32 rescoring of the kept band + sort
+    compact16<C>(kq, sm, qs, K, emb, cand + (int64_t)qid * K);
     // overflowed: listed for the exact-mode relaunch with its band limit as the seed (same list position)
-    if (npieces == 1) {
-      if (lane == 0 && sm.ovf[qs]) {
-        const int pos = atomicAdd(n_ovf, 1);
-        ovf_list[pos] = qid;
-        reinterpret_cast<uint32_t*>(n_ovf + 1)[pos] = (uint32_t)sm.ovf[qs];
-      }
-    } else if (lane == 0) {
-      kq[C - 1] = (uint64_t)(uint32_t)sm.ovf[qs];  // 0, or the flag's band-limit key
+    if (lane == 0 && sm.ovf[qs]) {
+      const int pos = atomicAdd(n_ovf, 1);
+      ovf_list[pos] = qid;
+      reinterpret_cast<uint32_t*>(n_ovf + 1)[pos] = (uint32_t)sm.ovf[qs];
     }
   }
   if (ABL && sink == 0x7fffffff) cand[0] = sink;
@@ -1397,16 +1461,21 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
   }
 }
 
-// Merge the pieces of split blocks: per query, the P sorted exact top-K key lists of its block's pieces → the
-// top K of their union (the top K of a union is the top K of the parts' top Ks), ties by index as everywhere.
-// One wave per query; a query flagged by any piece goes to the exact-mode relaunch list once, with the largest seed.
-template <int C, int QB>
+// Merge the pieces of split blocks: per query, the union of its P pieces' bands (piece_band: entries whose key beats
+// the shared limit at the piece's end) is filtered once more by the query's final shared limit Lk, rescored in exact
+// f32 (sgemv16, the order of every other final pass), sorted (score desc, index asc) and cut to K.  Every exact top-K
+// member lies in one piece's chunk range with a key above every limit, so it is in the union; the piece that
+// published Lk holds K entries above it, so the union has at least K whenever Lk != 0.  A query flagged by any piece,
+// or whose union would not fit one sort (C entries), goes to the exact-mode relaunch list once, seeded with the
+// largest flag key (each a valid band limit) or Lk.  One wave per query.
+template <int C, int QB, bool HL>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
                                                       const int32_t* __restrict__ n_active_p, int plan_rt, int plan_p,
                                                       int K, int32_t* __restrict__ cand, int32_t* __restrict__ ovf_list,
-                                                      int32_t* __restrict__ n_ovf) {
-  constexpr int E = kMaxPieces;  // ≤ 8 pieces × K ≤ 64 keys = 512 = 8 per lane
+                                                      int32_t* __restrict__ n_ovf, const uint32_t* __restrict__ share,
+                                                      const float* __restrict__ emb, int64_t q_offset) {
+  constexpr int E = C / 64;
   const int n_active = *n_active_p;
   const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // split-block query index
@@ -1417,35 +1486,109 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   const int64_t qq = slot_query(block, ql, plan.nb, QB);
   if (qq >= n_active) return;
   const int P = plan.P;
+  const uint64_t* kqs[kMaxPieces];
+  int cnt[kMaxPieces + 1];  // prefix of the pieces' band counts
+  uint32_t seed = 0u;
+  cnt[0] = 0;
+#pragma unroll
+  for (int p = 0; p < kMaxPieces; ++p) {
+    const int64_t item = plan.F + (block - plan.F) * P + (p < P ? p : 0);
+    kqs[p] = gkeys_all + ((size_t)item * QB + ql) * C;
+    const uint64_t hdr = p < P ? kqs[p][C - 1] : 0ull;
+    seed = max(seed, (uint32_t)(hdr >> 32));
+    cnt[p + 1] = cnt[p] + (int)(uint32_t)hdr;
+  }
+  const int n = cnt[kMaxPieces];
+  const uint32_t Lk = share[qq];
+  const int32_t qid = active[qq];
+  // Stage the union (entries above the shared limit) in the wave's LDS row, take its K-th largest key T by a greedy
+  // bitwise select and keep the band above T − margin (the pieces' own limits only know their local K-th, which for
+  // many pieces lies far below the query's)
+  constexpr int kU = (C - 64) * kMaxPieces / 64;  // union entries per lane at most
+  __shared__ uint64_t stage[4][(C - 64) * kMaxPieces];
+  uint64_t* sw = stage[threadIdx.x >> 6];
+  int m = 0;
+  for (int e0 = 0; e0 < n && seed == 0u; e0 += 64) {
+    const int e = e0 + lane;
+    int p = 0;
+#pragma unroll
+    for (int pp = 1; pp < kMaxPieces; ++pp) p += e >= cnt[pp] ? 1 : 0;
+    const uint64_t x = e < n ? kqs[p][e - cnt[p]] : 0ull;
+    const bool keep = x != 0ull && (uint32_t)(x >> 32) > Lk;
+    const uint64_t bm = __ballot(keep);
+    const int pos = m + __popcll(bm & ((1ull << lane) - 1ull));
+    if (keep) sw[pos] = x;
+    m += __popcll(bm);
+  }
+  uint32_t L = Lk;
+  if (seed == 0u && m > K) {
+    uint32_t hk[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = u * 64 + lane;
+      hk[u] = e < m ? (uint32_t)(sw[e] >> 32) : 0u;
+    }
+    uint32_t T = 0;
+    for (int bit = 31; bit >= (HL ? 0 : 12); --bit) {
+      const uint32_t Tc = T | (1u << bit);
+      int c = 0;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) c += __popcll(__ballot(hk[u] >= Tc));
+      if (c >= K) T = Tc;
+    }
+    L = max(L, f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta));
+  }
+  // the band above L, compacted in place at the front of the row (a round's reads precede its writes, which land
+  // below the round), then into v (slot j·64 + lane)
+  int mb = 0;
+  for (int e0 = 0; e0 < m && seed == 0u; e0 += 64) {
+    const int e = e0 + lane;
+    const uint64_t x = e < m ? sw[e] : 0ull;
+    const bool keep = x != 0ull && (uint32_t)(x >> 32) > L;
+    const uint64_t bm = __ballot(keep);
+    const int pos = mb + __popcll(bm & ((1ull << lane) - 1ull));
+    if (keep) sw[pos] = x;
+    mb += __popcll(bm);
+  }
   uint64_t v[E];
-  uint32_t seed = 0u;  // overflow: max over the pieces of their band-limit keys (each a valid lower bound); 0 = none
 #pragma unroll
   for (int j = 0; j < E; ++j) {
-    // slot j·64 + lane ↔ piece (j·64 + lane) / K, entry (j·64 + lane) % K
     const int e = j * 64 + lane;
-    const int p = e / K, r = e % K;
-    v[j] = 0ull;
-    if (p < P) {
-      const int64_t item = plan.F + (block - plan.F) * P + p;
-      const uint64_t* kq = gkeys_all + ((size_t)item * QB + ql) * C;
-      v[j] = kq[r];
-      if (r == 0) seed = max(seed, (uint32_t)kq[C - 1]);
+    v[j] = e < mb && e < C ? sw[e] : 0ull;
+  }
+  if (seed != 0u || mb > C) {
+    if (lane == 0) {
+      const int pos = atomicAdd(n_ovf, 1);
+      ovf_list[pos] = qid;
+      reinterpret_cast<uint32_t*>(n_ovf + 1)[pos] = max(seed, L);
     }
+    return;
+  }
+  const float4* qp = reinterpret_cast<const float4*>(emb + ((int64_t)qid + q_offset) * 16);
+  float qv[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 x = qp[i];
+    qv[4 * i] = x.x; qv[4 * i + 1] = x.y; qv[4 * i + 2] = x.z; qv[4 * i + 3] = x.w;
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) seed = max(seed, (uint32_t)__shfl_xor((int)seed, o));
+  for (int j = 0; j < E; ++j) {
+    if (v[j] != 0ull) {
+      const int32_t d = key_idx(v[j]);
+      const float4* rp = reinterpret_cast<const float4*>(emb + (int64_t)d * 16);
+      float4 row[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) row[i] = rp[i];
+      const float acc = sgemv16([&](int k) { return f4c(row[k >> 2], k & 3); }, [&](int k) { return qv[k]; });
+      v[j] = make_key(acc, d);
+    }
+  }
   wave_sort_desc<E>(v);
-  const int32_t qid = active[qq];
   int32_t* out = cand + (int64_t)qid * K;
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
     if (e < K) out[e] = v[j] != 0ull ? key_idx(v[j]) : -1;
-  }
-  if (seed != 0u && lane == 0) {
-    const int pos = atomicAdd(n_ovf, 1);
-    ovf_list[pos] = qid;
-    reinterpret_cast<uint32_t*>(n_ovf + 1)[pos] = seed;
   }
 }
 
@@ -1563,7 +1706,8 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     const int64_t q1 = max_q > 0 ? max_q : 1;
     // workspace tail: two overflow lists, each list[q], count, seeds u32[q] (seeds[i] = f2key of the band limit of
     // list[i]); the first pass's list is the last block of the workspace
-    int32_t* ovf2 = (int32_t*)((char*)gkeys + keys_bytes);
+    uint32_t* share = (uint32_t*)((char*)gkeys + keys_bytes);  // u32[q]: shared band limits of split blocks
+    int32_t* ovf2 = (int32_t*)(share + q1);
     int32_t* n_ovf2 = ovf2 + q1;
     int32_t* ovf1 = n_ovf2 + 1 + q1;
     int32_t* n_ovf1 = ovf1 + q1;
@@ -1579,13 +1723,14 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     int rt, P;
     host_plan_for(max_q, nd, wide, rt, P);
     const TopkPlan pl = make_plan(max_q, rt, P, wide ? kWideQB : k16QB);
+    if (pl.R > 0 && !pl.halves) (void)hipMemsetAsync(share, 0, (size_t)q1 * sizeof(uint32_t), st);
     const int mode1 = first_mode(nd);
 #define FWAV_FIRST(MODE_, STATS_, DBG_, ST_)                                                                    \
   k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, 0, st>>>(                                 \
-      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, nullptr, 0.0f, rt, P, DBG_, ST_)
+      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, DBG_, ST_)
 #define FWAV_FIRST_WIDE(MODE_)                                                                                   \
   k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG><<<pl.items(), 64 * kWideW, 0, st>>>(                    \
-      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, nullptr, 0.0f, rt, P, 0, nullptr)
+      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr)
 #ifdef FWAV_TOPK_EXTSEED
     if (stats != nullptr && dbg == 0) {
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
@@ -1602,12 +1747,15 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
 #undef FWAV_FIRST
 #undef FWAV_FIRST_WIDE
     if (pl.R > 0) {
-      if (wide)
-        k_merge_pieces<k16Cap, kWideQB><<<cdiv(pl.R * kWideQB, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K,
-                                                                               cand, ovf1, n_ovf1);
-      else
-        k_merge_pieces<k16Cap, k16QB><<<cdiv(pl.R * k16QB, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand,
-                                                                            ovf1, n_ovf1);
+#define FWAV_MERGE(QB_, HL_)                                                                                    \
+  k_merge_pieces<k16Cap, QB_, HL_><<<cdiv(pl.R * QB_, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, \
+                                                                       ovf1, n_ovf1, share, emb, q_offset)
+      if (wide) {
+        if (mode1 == kModeHL) FWAV_MERGE(kWideQB, true); else FWAV_MERGE(kWideQB, false);
+      } else {
+        if (mode1 == kModeHL) FWAV_MERGE(k16QB, true); else FWAV_MERGE(k16QB, false);
+      }
+#undef FWAV_MERGE
     }
     // Queries whose band overflowed the buffer (large groups of equal or nearly equal scores) are searched again by
     // the same kernel in a narrower mode, on the device-side overflow list (no host sync; a relaunch exits at once
@@ -1619,7 +1767,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     const uint32_t* ex_seeds = seeds1;
     if (mode1 == kModeS16) {
       k_sim_topk_f16<k16Cap, false, kModeHL><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, ovf1, n_ovf1, q_offset, K, cand, gkeys, ovf2, n_ovf2, seeds1, kStreamMargin, 0, 1, 0,
+          emb16, emb, nd, ovf1, n_ovf1, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, seeds1, kStreamMargin, 0, 1, 0,
           nullptr);
       ex_in = ovf2;
       ex_n = n_ovf2;
@@ -1627,11 +1775,11 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     }
     if (stats != nullptr && (dbg & (1 << 17)))  // diagnostic: counters of the exact-mode relaunch only
       k_sim_topk_f16<k16Cap, true, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, ex_seeds, kStreamMargin, 0, 1, 0,
+          emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, ex_seeds, kStreamMargin, 0, 1, 0,
           stats);
     else
       k_sim_topk_f16<k16Cap, false, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
-          emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, ex_seeds, kStreamMargin, 0, 1, 0,
+          emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, ex_seeds, kStreamMargin, 0, 1, 0,
           nullptr);
   } else {
     const size_t lds = topk_lds_bytes<C>();
@@ -1666,7 +1814,7 @@ int fwav_topk_max_k(void) { return 4096; }
 size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   const int64_t q = max_q > 0 ? max_q : 1;
   if (k > 64) return large_workspace_bytes(n_domains, q);
-  return f16_keys_bytes(q, n_domains) + 2 * (size_t)(2 * q + 1) * sizeof(int32_t);
+  return f16_keys_bytes(q, n_domains) + (size_t)q * sizeof(uint32_t) + 2 * (size_t)(2 * q + 1) * sizeof(int32_t);
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,

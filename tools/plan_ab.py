@@ -49,13 +49,15 @@ for rnd in range(3):
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
+        o = wsn - 4 - 4 * max(nq, 1)  # workspace tail: first pass's overflow list, its count, then u32 seeds[q]
+        n_ovf = int(wsk[o:o + 4].view(torch.int32).item())
         if ref is None:
             ref = cand.clone()
         same = bool(torch.equal(cand, ref))
         if rnd == 2:
-            res.append((rt, P, np.median(ts), min(ts), same, wsn))
+            res.append((rt, P, np.median(ts), min(ts), same, wsn, n_ovf))
         del wsk
 call("fwav_debug_topk_plan", -1, 1)
-for rt, P, med, mn, same, wsn in res:
-    print(f"plan rt={rt:5d} P={P}: median {med:7.2f} ms  min {mn:7.2f}  identical={same}  workspace {wsn / 2**30:.2f} GiB",
+for rt, P, med, mn, same, wsn, n_ovf in res:
+    print(f"plan rt={rt:5d} P={P}: median {med:7.2f} ms  min {mn:7.2f}  identical={same}  workspace {wsn / 2**30:.2f} GiB  overflowed {n_ovf}",
           flush=True)

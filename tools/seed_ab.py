@@ -31,14 +31,19 @@ ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
      emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
-active = torch.arange(nr, dtype=torch.int32, device="cuda")
-n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
-wsn = L.fwav_sim_topk_workspace_size(nr, nd, 64)
+nq = int(os.environ.get("AB_NQ", nr))  # the first nq ranges (one rank's share at N > 1)
+active = torch.arange(nq, dtype=torch.int32, device="cuda")
+n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
+wsn = L.fwav_sim_topk_workspace_size(nq, nd, 64)
 wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
 E = emb.view(nd, 16)
 ref = None
 for S in [0] + [int(x) for x in sys.argv[2:]]:
     seeds = torch.full((nr,), -float("inf"), device="cuda")
+    if S < 0:  # ideal: the exact K-th best score of every query (from the search's own candidates), minus 3δ
+        # (S = -1), or minus (-S)/1000 more (S = -20: 0.020 below the ideal seed)
+        kth = r.cand.view(nr, 64)[:, 63].long()
+        seeds = ((E[:nr].double() * E[kth].double()).sum(1) - 3 * 2.0e-3 - (0 if S == -1 else -S / 1000.0)).float()
     if S > 0:
         samp = torch.linspace(0, nd - 1, S, device="cuda").long()
         Es = E[samp].double()
@@ -51,14 +56,15 @@ for S in [0] + [int(x) for x in sys.argv[2:]]:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        rc = L.fwav_debug_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
+        rc = L.fwav_debug_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
                                    64, cand.data_ptr(), wsk.data_ptr(), 0, seeds.data_ptr(), st)
         e1.record()
         torch.cuda.synchronize()
         assert rc == 0
         if rep:
             times.append(e0.elapsed_time(e1))
+    cand = cand[:nq * 64]
     if ref is None:
         ref = cand.clone()
-    print(f"sample {S:6d}: median {np.median(times):7.2f} ms  seed mean {seeds[seeds > -1e30].mean().item() if S else float('nan'):.4f}"
+    print(f"sample {S:6d} (-1 = ideal): median {np.median(times):7.2f} ms  seed mean {seeds[seeds > -1e30].mean().item() if S else float('nan'):.4f}"
           f"  identical={bool(torch.equal(cand, ref))}", flush=True)

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""One rank's share of the sharded cfg2 compress, on one GPU (diagnostic for strong scaling): the step time of
+compress_device(sig, shard=(0, nr/N)) for N = 1, 2, 4, 8 — everything a rank of bench.py --gpus N does except the
+collectives — with per-stage HIP events and the host wall time per step.
+usage: python tools/shard_step.py [--steps 20]"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "audio-compression_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--config", default="cfg2")
+    a = ap.parse_args()
+    import __graft_entry__
+    __graft_entry__.build()
+    from fwav import dist as fdist
+    from fwav import engine, synth
+    dev = torch.device("cuda", 0)
+    cfg = synth.CONFIGS[a.config]
+    sig_h, _, _ = synth.make_config_signal(a.config, seed=0)
+    sig = torch.from_numpy(sig_h).to(dev)
+    tile, K = cfg["tile"], cfg["top_k"]
+    out = {}
+    for N in (1, 2, 4, 8):
+        def shard(ranges, n_ranges, range_size, N=N):
+            return fdist.prune_balanced_bounds(ranges, n_ranges, range_size, 1e-4, N)[0]
+        for _ in range(2):
+            engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard)
+        torch.cuda.synchronize()
+        evs = []
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            ev = {}
+            r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard, events=ev)
+            evs.append(ev)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / a.steps * 1e3
+        st = {k: float(np.mean([e[k][0].elapsed_time(e[k][1]) for e in evs])) for k in evs[0]}
+        out[N] = {"ranges": r.shard[1] - r.shard[0], "wall_ms": wall, "stage_ms": st,
+                  "gpu_sum_ms": sum(st.values())}
+        print(N, json.dumps(out[N]), flush=True)
+    base = out[1]["wall_ms"]
+    print(json.dumps({N: {"speedup_wall": base / v["wall_ms"]} for N, v in out.items()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
