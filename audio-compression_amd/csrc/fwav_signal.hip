@@ -161,25 +161,85 @@ __global__ void k_form_ranges(const float* __restrict__ sig, int64_t n, int fram
 // recursion.  Phase 2: one lane adds the buffer sums in order.
 constexpr int kNpBuf = 8192;
 
-__device__ float pw_sq_rec(const float* __restrict__ x, int n) {
-  auto sq = [&](int i) { return x[i] * x[i]; };
-  // depth: 8191 → ≤ 6 halvings to reach ≤ 128
-  return pw_rec<7>(sq, 0, n);
+// The leaves of numpy's pairwise recursion over n elements (pw_rec's splits), in order: offsets and lengths.
+// Depth: 8191 → ≤ 6 halvings to reach ≤ 128.
+template <int D>
+__device__ void pw_leaf_list(int off, int n, int* loff, int* llen, int& k) {
+  if constexpr (D > 0) {
+    if (n > 128) {
+      int n2 = n / 2;
+      n2 -= n2 % 8;
+      pw_leaf_list<D - 1>(off, n2, loff, llen, k);
+      pw_leaf_list<D - 1>(off + n2, n - n2, loff, llen, k);
+      return;
+    }
+  }
+  loff[k] = off;
+  llen[k] = n;
+  ++k;
+}
+// The same recursion with the leaves' sums given (in order): left + right at every node.
+template <int D>
+__device__ float pw_tree_from_leaves(int n, const float* lsum, int& k) {
+  if constexpr (D > 0) {
+    if (n > 128) {
+      int n2 = n / 2;
+      n2 -= n2 % 8;
+      const float a = pw_tree_from_leaves<D - 1>(n2, lsum, k);
+      const float c = pw_tree_from_leaves<D - 1>(n - n2, lsum, k);
+      return a + c;
+    }
+  }
+  return lsum[k++];
 }
 
-__global__ void k_energy_buffers(const float* __restrict__ x, int64_t n, float* __restrict__ bufsum) {
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int64_t nb = cdiv(n, kNpBuf);
-  if (b >= nb) return;
+// One 256-thread workgroup per full buffer: the 8192 elements are loaded coalesced (two float4 per thread and step)
+// into LDS, leaf-major with a one-float skew (leaf l at l·129, so the 64 lanes reading element i of their leaves hit
+// 64 different banks), then wave 0 evaluates one leaf per lane and combines the 64 leaves by shuffles.  (Reading the
+// leaves straight from global memory, lane l at x[128 l + i], touched 64 lines per load: 161 µs at cfg2.)
+constexpr int kLeafSkew = 129;
+__global__ __launch_bounds__(256) void k_energy_buffers(const float* __restrict__ x, int64_t n,
+                                                        float* __restrict__ bufsum) {
+  __shared__ float lds[64 * kLeafSkew];
+  const int64_t b = blockIdx.x;
   const int64_t off = b * kNpBuf;
   const int64_t len = n - off < kNpBuf ? n - off : kNpBuf;
-  if (len < kNpBuf) {  // the partial last buffer: general pairwise recursion, one lane
-    if (lane == 0) bufsum[b] = pw_sq_rec(x + off, (int)len);
+  const int lane = threadIdx.x & 63;
+  if (len < kNpBuf) {
+    // the partial last buffer: the pairwise recursion's leaves (≤ 128 of ≤ 128 elements) are listed by one lane,
+    // summed one per thread, and combined in the recursion's order by one lane (evaluating the whole recursion on one
+    // lane took ≈ 160 µs at cfg2)
+    __shared__ int loff[128], llen[128], nleaf;
+    __shared__ float lsum[128];
+    if (threadIdx.x == 0) {
+      int k = 0;
+      pw_leaf_list<7>(0, (int)len, loff, llen, k);
+      nleaf = k;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nleaf; i += blockDim.x) {
+      const float* p = x + off + loff[i];
+      lsum[i] = pw_leaf([&](int j) { return p[j] * p[j]; }, 0, llen[i]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int k = 0;
+      bufsum[b] = pw_tree_from_leaves<7>((int)len, lsum, k);
+    }
     return;
   }
-  // full buffer: 8192 = 64 leaves of 128 (every split of 8192 … 256 is exactly in half)
-  const float* leaf = x + off + lane * 128;
+  const float4* x4 = reinterpret_cast<const float4*>(x + off);
+#pragma unroll
+  for (int k = 0; k < kNpBuf / 4 / 256; ++k) {
+    const int e4 = k * 256 + threadIdx.x;  // float4 index: elements 4·e4 .. 4·e4 + 3, all in leaf (4·e4) / 128
+    const float4 v = x4[e4];
+    const int e = 4 * e4, leaf = e >> 7, pos = e & 127;
+    float* d = lds + leaf * kLeafSkew + pos;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const float* leaf = lds + lane * kLeafSkew;
   float v = pw_leaf([&](int i) { return leaf[i] * leaf[i]; }, 0, 128);
 #pragma unroll
   for (int w = 1; w < 64; w <<= 1) {
@@ -189,11 +249,17 @@ __global__ void k_energy_buffers(const float* __restrict__ x, int64_t n, float* 
   if (lane == 0) bufsum[b] = v;
 }
 
+// The buffer sums added in order into the f32 accumulator: one wave loads 64 sums at a time, lane 0's chain adds them
+// in order (readlane).
 __global__ void k_energy_chain(const float* __restrict__ bufsum, int64_t nb, float* __restrict__ out) {
-  if (threadIdx.x != 0) return;
+  const int lane = threadIdx.x & 63;
   float acc = 0.0f;
-  for (int64_t b = 0; b < nb; ++b) acc = acc + bufsum[b];
-  out[0] = acc;
+  for (int64_t c = 0; c < nb; c += 64) {
+    const float v = c + lane < nb ? bufsum[c + lane] : 0.0f;
+    const int m = nb - c < 64 ? (int)(nb - c) : 64;
+    for (int j = 0; j < m; ++j) acc = acc + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+  }
+  if (lane == 0) out[0] = acc;
 }
 
 // Energy prune + degenerate queries + active list (fractal.py:598-622, quirk Q1/Q3/Q11).
@@ -316,10 +382,11 @@ int fwav_weighted_energy(const float* ranges, int64_t n, float* sum, void* works
   FWAV_CHECK_ARG(ranges && sum && n >= 0, FWAV_ERR_ARG, "fwav_weighted_energy: bad args");
   FWAV_CHECK_ARG(workspace && ws_bytes >= fwav_weighted_energy_workspace_size(n), FWAV_ERR_WORKSPACE,
                  "fwav_weighted_energy: workspace too small");
+  FWAV_CHECK_ARG(((uintptr_t)ranges & 15) == 0, FWAV_ERR_ARG, "fwav_weighted_energy: ranges must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
   const int64_t nb = cdiv(n, kNpBuf);
   float* bufsum = (float*)workspace;
-  if (nb > 0) k_energy_buffers<<<cdiv(nb, 4), 256, 0, st>>>(ranges, n, bufsum);
+  if (nb > 0) k_energy_buffers<<<nb, 256, 0, st>>>(ranges, n, bufsum);
   k_energy_chain<<<1, 64, 0, st>>>(bufsum, nb, sum);
   FWAV_LAUNCH_CHECK("fwav_weighted_energy");
   return FWAV_OK;

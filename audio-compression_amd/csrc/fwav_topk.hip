@@ -1501,60 +1501,58 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   const int n = cnt[kMaxPieces];
   const uint32_t Lk = share[qq];
   const int32_t qid = active[qq];
-  // Stage the union (entries above the shared limit) in the wave's LDS row, take its K-th largest key T by a greedy
-  // bitwise select and keep the band above T − margin (the pieces' own limits only know their local K-th, which for
-  // many pieces lies far below the query's)
+  // Load the union (entries above the shared limit) into registers, all loads issued together, take its K-th largest
+  // key T by a greedy bitwise select and keep the band above T − margin (the pieces' own limits only know their local
+  // K-th, which for many pieces lies far below the query's)
   constexpr int kU = (C - 64) * kMaxPieces / 64;  // union entries per lane at most
-  __shared__ uint64_t stage[4][(C - 64) * kMaxPieces];
-  uint64_t* sw = stage[threadIdx.x >> 6];
-  int m = 0;
-  for (int e0 = 0; e0 < n && seed == 0u; e0 += 64) {
-    const int e = e0 + lane;
+  const int nu = (n + 63) >> 6;                   // registers in use (wave-uniform)
+  uint64_t x[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    x[u] = 0ull;
+    if (u >= nu || seed != 0u) continue;
+    const int e = u * 64 + lane;
     int p = 0;
 #pragma unroll
     for (int pp = 1; pp < kMaxPieces; ++pp) p += e >= cnt[pp] ? 1 : 0;
-    const uint64_t x = e < n ? kqs[p][e - cnt[p]] : 0ull;
-    const bool keep = x != 0ull && (uint32_t)(x >> 32) > Lk;
-    const uint64_t bm = __ballot(keep);
-    const int pos = m + __popcll(bm & ((1ull << lane) - 1ull));
-    if (keep) sw[pos] = x;
-    m += __popcll(bm);
+    const uint64_t y = e < n ? kqs[p][e - cnt[p]] : 0ull;
+    x[u] = (uint32_t)(y >> 32) > Lk ? y : 0ull;
   }
+  int m = 0;
+#pragma unroll
+  for (int u = 0; u < kU; ++u)
+    if (u < nu) m += __popcll(__ballot(x[u] != 0ull));
   uint32_t L = Lk;
   if (seed == 0u && m > K) {
-    uint32_t hk[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = u * 64 + lane;
-      hk[u] = e < m ? (uint32_t)(sw[e] >> 32) : 0u;
-    }
     uint32_t T = 0;
     for (int bit = 31; bit >= (HL ? 0 : 12); --bit) {
       const uint32_t Tc = T | (1u << bit);
       int c = 0;
 #pragma unroll
-      for (int u = 0; u < kU; ++u) c += __popcll(__ballot(hk[u] >= Tc));
+      for (int u = 0; u < kU; ++u)
+        if (u < nu) c += __popcll(__ballot((uint32_t)(x[u] >> 32) >= Tc));
       if (c >= K) T = Tc;
     }
     L = max(L, f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta));
   }
-  // the band above L, compacted in place at the front of the row (a round's reads precede its writes, which land
-  // below the round), then into v (slot j·64 + lane)
+  // the band above L, compacted into the wave's LDS row, then into v (slot j·64 + lane)
+  __shared__ uint64_t stage[4][C];
+  uint64_t* sw = stage[threadIdx.x >> 6];
   int mb = 0;
-  for (int e0 = 0; e0 < m && seed == 0u; e0 += 64) {
-    const int e = e0 + lane;
-    const uint64_t x = e < m ? sw[e] : 0ull;
-    const bool keep = x != 0ull && (uint32_t)(x >> 32) > L;
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    if (u >= nu) break;
+    const bool keep = x[u] != 0ull && (uint32_t)(x[u] >> 32) > L;
     const uint64_t bm = __ballot(keep);
     const int pos = mb + __popcll(bm & ((1ull << lane) - 1ull));
-    if (keep) sw[pos] = x;
+    if (keep && pos < C) sw[pos] = x[u];
     mb += __popcll(bm);
   }
   uint64_t v[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
-    v[j] = e < mb && e < C ? sw[e] : 0ull;
+    v[j] = e < mb && e < C ? sw[e] : 0ull;  // same wave: its own ds_writes are ordered before these reads
   }
   if (seed != 0u || mb > C) {
     if (lane == 0) {
@@ -1663,6 +1661,12 @@ static void host_plan_for(int64_t max_q, int64_t nd, bool wide, int& rt, int& P)
       const int64_t last = nb % slots == 0 ? slots : nb % slots;  // blocks in the last round
       if (last > cus) {
         rt = (int)(2 * (last - cus) < nb ? 2 * (last - cus) : nb);
+        P = 4;
+      } else if (5 * last <= 3 * cus) {
+        // a last round of lone workgroups on at most 60 % of the CUs: its blocks as 4 table pieces each.  Same-box
+        // A/B (identical outputs), last-round blocks → ms unsplit / split: 60 → 12.45 / 9.39, 134 (one rank's half
+        // of cfg2) 12.54 / 11.24, 200 12.60 / 12.74, 250 13.13 / 13.33
+        rt = (int)last;
         P = 4;
       }
     }

@@ -49,7 +49,8 @@ int fwav_voiced_ranges(const float* sig, int64_t n, int range_size, int frame, i
                        void* stream);
 
 /* Silent-input test of compress_audio (fractal.py:1083): sum[0] = np.sum(ranges[0:n] ** 2) in float32, bit-exact
- * (numpy's 8192-element reduction buffers, each a pairwise sum); the caller compares it with float32(1e-8). */
+ * (numpy's 8192-element reduction buffers, each a pairwise sum); the caller compares it with float32(1e-8).
+ * ranges must be 16-B aligned. */
 size_t fwav_weighted_energy_workspace_size(int64_t n);
 int fwav_weighted_energy(const float* ranges, int64_t n, float* sum, void* workspace, size_t ws_bytes, void* stream);
 

@@ -1,0 +1,51 @@
+"""Counters of the fp16 search's first pass (STATS build of the kernel: replayed chunks, firing tiles, appends,
+compactions, time shares) on cfg2 for the first AB_NQ queries (tools only).
+usage: AB_NQ=41344 python tools/first_stats.py"""
+import os
+import sys
+
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd")]
+import torch
+
+import __graft_entry__
+
+__graft_entry__.build()
+from fwav import engine, synth  # noqa: E402
+from fwav._lib import call, size_call  # noqa: E402
+
+sig_h, _, _ = synth.make_config_signal("cfg2")
+sig = torch.from_numpy(sig_h).cuda()
+r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
+torch.cuda.synchronize()
+nd, nr = r.n_domains, r.n_ranges
+st = torch.cuda.current_stream().cuda_stream
+emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
+tab = engine.embed_tables(8, torch.device("cuda"))
+pool = torch.empty(nd * 8, device="cuda")
+emb = torch.empty(nd * 16, device="cuda")
+ws = torch.empty(max(size_call("fwav_pool_workspace_size", sig.numel(), 2048, 8, 2), 16), dtype=torch.uint8,
+                 device="cuda")
+call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
+     emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+nq = int(os.environ.get("AB_NQ", nr))
+active = torch.arange(nq, dtype=torch.int32, device="cuda")
+n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
+wsn = size_call("fwav_sim_topk_workspace_size", nq, nd, 64)
+wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
+cand = torch.empty(nq * 64, dtype=torch.int32, device="cuda")
+for rep in range(2):
+    stats = torch.zeros(16, dtype=torch.int64, device="cuda")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
+         64, cand.data_ptr(), wsk.data_ptr(), 0, stats.data_ptr(), st)
+    e1.record()
+    torch.cuda.synchronize()
+    sv = stats.cpu().tolist()
+    qsets = max((nq + 31) // 32, 1)
+    tot = max(sv[6], 1)
+    print(f"rep {rep}: {e0.elapsed_time(e1):.2f} ms (STATS build); per query set of 32: replayed chunks "
+          f"{sv[0] / qsets:.0f}, firing tiles {sv[1] / qsets:.0f}; per query: appends {sv[2] / nq:.1f}, compactions "
+          f"{sv[3] / nq:.2f}; shares: barrier {sv[7] / tot:.3f} streaming {sv[9] / tot:.3f} replays {sv[4] / tot:.3f} "
+          f"(appends {sv[10] / tot:.3f}) final {sv[8] / tot:.3f}", flush=True)
