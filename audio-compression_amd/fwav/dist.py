@@ -74,13 +74,16 @@ def prune_balanced_bounds(ranges: torch.Tensor, n_ranges: int, range_size: int, 
     mean(r²) clears float32(0.75·thr) costs one full-table search (weight 1024), a pruned one almost nothing
     (weight 1).  Integer weights and an integer cumsum, so every rank derives the same bounds from its own
     (bit-identical) ranges with no collective.  Scheduling only: the exact prune runs inside each rank's search."""
+    if world == 1 or n_ranges == 0:
+        return [(0, n_ranges)] + [(n_ranges, n_ranges)] * (world - 1)
     x = ranges[:n_ranges * range_size].view(n_ranges, range_size)
     thr = float(np.float32(energy_thresh * 0.75))
     active = (x.double().square().mean(dim=1) >= thr).to(torch.int64)
     cs = torch.cumsum(active * 1023 + 1, dim=0)
-    total = int(cs[-1].item()) if n_ranges else 0
-    targets = torch.tensor([total * r // world for r in range(1, world)], dtype=torch.int64, device=cs.device)
-    cuts = torch.searchsorted(cs, targets, right=True).cpu().tolist() if world > 1 else []
+    # targets total·r // world on the device: one host synchronisation (the cut positions)
+    r = torch.arange(1, world, dtype=torch.int64, device=cs.device)
+    targets = torch.div(cs[-1] * r, world, rounding_mode="floor")
+    cuts = torch.searchsorted(cs, targets, right=True).cpu().tolist()
     cuts = [0] + [min(int(c), n_ranges) for c in cuts] + [n_ranges]
     cuts = np.maximum.accumulate(cuts)
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
@@ -122,28 +125,36 @@ def _device_compute(sig, tile_size, top_k, energy_thresh, shard):
 
 def compress_sharded_device(sig: Optional[torch.Tensor], tile_size: int, top_k: int, energy_thresh: float = 1e-4,
                             group=None, device: Optional[torch.device] = None, compute: Optional[Callable] = None,
-                            timings: Optional[dict] = None):
+                            timings: Optional[dict] = None, n: Optional[int] = None):
     """The sharded compress on device tensors.  ``sig`` (1-D f32, on ``device``) is needed on rank 0 only.
     Returns on rank 0 a dict of full-length device tensors idx/s/o/sym/err, the pool, the blocks and geometry;
-    None on the other ranks.  ``timings`` (if given) receives per-phase host seconds (broadcast / compute /
-    gather), each phase closed by a device synchronisation."""
+    None on the other ranks.  ``n`` (the signal length, if every rank knows it) saves broadcasting it.
+    ``timings`` (if given) receives per-phase host seconds (broadcast / compute / gather), each phase then closed by
+    a device synchronisation (without it the phases run back to back, with no synchronisation of their own)."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     compute = compute or _device_compute
     tm = timings if timings is not None else {}
+    timed = timings is not None
+
+    def mark():
+        if timed:
+            _sync(device)
+        return time.perf_counter()
+
     t0 = time.perf_counter()
-    n_t = torch.zeros(1, dtype=torch.int64, device=device)
-    if rank == 0:
-        n_t[0] = int(sig.numel())
-    _broadcast_(n_t, group, device)
-    n = int(n_t.item())
+    if n is None:
+        n_t = torch.zeros(1, dtype=torch.int64, device=device)
+        if rank == 0:
+            n_t[0] = int(sig.numel())
+        _broadcast_(n_t, group, device)
+        n = int(n_t.item())
     if rank != 0:
         sig = torch.empty(n, dtype=torch.float32, device=device)
     _broadcast_(sig, group, device)  # the one data-path collective before the search
-    _sync(device)
-    t1 = time.perf_counter()
+    t1 = mark()
 
     rs, step = geometry(tile_size)
     nr = -(-n // rs)
@@ -154,8 +165,7 @@ def compress_sharded_device(sig: Optional[torch.Tensor], tile_size: int, top_k: 
         return blocks_box[rank]
 
     res = compute(sig, tile_size, top_k, energy_thresh, shard)
-    _sync(device)
-    t2 = time.perf_counter()
+    t2 = mark()
     if res is None:  # empty / short / silent input: identical decision on every rank
         tm.update(broadcast_s=t1 - t0, compute_s=t2 - t1, gather_s=0.0)
         return dict(empty=True, n_ranges=0, range_size=rs, domain_step=step, original_len=n) if rank == 0 else None
@@ -165,8 +175,7 @@ def compress_sharded_device(sig: Optional[torch.Tensor], tile_size: int, top_k: 
     mine = _pack(res, maxlen, cd)
     glist = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
     dist.gather(mine, gather_list=glist, dst=0, group=group)
-    _sync(device)
-    t3 = time.perf_counter()
+    t3 = mark()
     tm.update(broadcast_s=t1 - t0, compute_s=t2 - t1, gather_s=t3 - t2)
     if rank != 0:
         return None

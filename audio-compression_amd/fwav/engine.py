@@ -207,12 +207,6 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
         if res.is_silent() or n < tile_size:
             return _empty(n, rs, tile_size, step, energy_thresh, k)
         raise ValueError("mmap length is greater than file size")  # quirk Q9 (fractal.py:1190-1195)
-    if callable(shard):  # multi-GPU: bounds chosen from the ranges themselves (fwav.dist balances the prune)
-        shard = shard(ranges, nr, rs)
-    lo, hi = (0, nr) if shard is None else (int(shard[0]), int(shard[1]))
-    if not (0 <= lo <= hi <= nr):
-        raise ValueError(f"bad shard {shard} for {nr} ranges")
-    res.shard = (lo, hi)
     tab = embed_tables(rs, dev)
     pool = torch.empty(nd * rs, dtype=torch.float32, device=dev)
     emb = torch.empty(nd * 16, dtype=torch.float32, device=dev)
@@ -227,6 +221,14 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     _mark(events, "pool_embed")
     if on_pool is not None:
         on_pool(pool)
+    # multi-GPU: bounds chosen from the ranges themselves (fwav.dist balances the prune); evaluated after the pool and
+    # embedding kernels are queued, so its host synchronisation overlaps them
+    if callable(shard):
+        shard = shard(ranges, nr, rs)
+    lo, hi = (0, nr) if shard is None else (int(shard[0]), int(shard[1]))
+    if not (0 <= lo <= hi <= nr):
+        raise ValueError(f"bad shard {shard} for {nr} ranges")
+    res.shard = (lo, hi)
     m = hi - lo
     cand = torch.empty(max(m, 1) * k, dtype=torch.int32, device=dev)
     active = torch.empty(max(m, 1), dtype=torch.int32, device=dev)

@@ -137,15 +137,18 @@ def main():
         def step(ev=None):
             return engine.compress_device(sig, tile, K, energy_thresh=1e-4, events=ev)
     else:
-        def step(ev=None):
+        def step(ev=None, phases=False):
             def compute(s, t, k, thr, shard):
                 r = engine.compress_device(s, t, k, energy_thresh=thr, shard=shard, events=ev)
                 step.last = r
                 return None if r.empty else dict(idx=r.idx, s=r.s, o=r.o, sym=r.sym, err=r.err, pool=r.pool,
                                                  silent=r.is_silent)
-            tm = {}
-            out = fdist.compress_sharded_device(sig, tile, K, 1e-4, device=dev, compute=compute, timings=tm)
-            for k_, v in tm.items():
+            # every rank knows the configuration's signal length; per-phase host timings (which synchronise the
+            # device at each phase boundary) are taken on an extra step after the timed ones
+            tm = {} if phases else None
+            out = fdist.compress_sharded_device(sig, tile, K, 1e-4, device=dev, compute=compute, timings=tm,
+                                                n=int(sig_h.size))
+            for k_, v in (tm or {}).items():
                 phase.setdefault(k_, []).append(v)
             step.out = out
             return step.last
@@ -175,6 +178,9 @@ def main():
     nr, nd, rs = res.n_ranges, res.n_domains, res.range_size
     per_rank = None
     if dist is not None:
+        for _ in range(3):  # phase breakdown (untimed)
+            step(phases=True)
+        torch.cuda.synchronize()
         cd = dev if backend == "nccl" else torch.device("cpu")
         t = torch.tensor([dt], dtype=torch.float64, device=cd)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
