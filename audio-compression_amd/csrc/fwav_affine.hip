@@ -327,11 +327,50 @@ __global__ __launch_bounds__(64 * kAffWaves) void k_affine_batch(const float* __
   }
 }
 
+// Diagnostic (bench roofline): the ceiling of the affine solver's memory side on this device — n uniformly random
+// rows of `rs` floats (16-B aligned) gathered from a table of nrows, 4 rows in flight per lane, nothing computed
+// (tools/micro/gather32.hip measured 44 G rows/s for 32-B rows of a 2.76 GB table: a request-rate limit).
+__device__ __forceinline__ uint32_t gather_hash(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+__global__ __launch_bounds__(256) void k_gather_rows(const float4* __restrict__ tab, uint32_t nrows, int q4, int64_t n,
+                                                     float* __restrict__ out) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float acc = 0.f;
+  for (int64_t i = tid * 4; i < n; i += stride * 4) {
+    float4 v[4][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t row = gather_hash((uint32_t)(i + b) * 2654435761u) % nrows;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < q4) v[b][k] = tab[(int64_t)row * q4 + k];
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < q4) acc += v[b][k].x;
+  }
+  if (acc == 1.2345f) out[0] = acc;
+}
+
 }  // namespace fwav
 
 using namespace fwav;
 
 extern "C" {
+
+int fwav_debug_gather_rows(const float* table, int64_t n_rows, int rs, int64_t n, float* sink, void* stream) {
+  FWAV_CHECK_ARG(table && sink && n_rows > 0 && n_rows < 0xffffffffLL && n >= 0 && (rs == 4 || rs == 8 || rs == 16),
+                 FWAV_ERR_ARG, "fwav_debug_gather_rows: bad args");
+  if (n == 0) return FWAV_OK;
+  k_gather_rows<<<8192, 256, 0, (hipStream_t)stream>>>((const float4*)table, (uint32_t)n_rows, rs / 4, n, sink);
+  FWAV_LAUNCH_CHECK("fwav_debug_gather_rows");
+  return FWAV_OK;
+}
 
 int fwav_affine(const float* ranges, int64_t nr, int rs, const int32_t* cand, int K, const float* pool, int64_t nd,
                 float s_clip, int32_t* out_idx, float* out_s, float* out_o, uint8_t* out_sym, float* out_err,

@@ -123,6 +123,10 @@ int fwav_debug_topk_geometry(int wide);
 int fwav_affine(const float* ranges, int64_t n_ranges, int range_size, const int32_t* cand, int k, const float* pool,
                 int64_t n_domains, float s_clip, int32_t* out_idx, float* out_s, float* out_o, uint8_t* out_sym,
                 float* out_err, void* stream);
+/* Diagnostic (bench roofline, not the product path): n uniformly random rows of rs floats (rs 4/8/16, 16-B aligned
+ * table of n_rows rows) gathered with nothing computed — the ceiling of fwav_affine's memory side on this device.
+ * sink: one float of device memory. */
+int fwav_debug_gather_rows(const float* table, int64_t n_rows, int rs, int64_t n, float* sink, void* stream);
 
 /* ------------------------------------------------------------------- decompression loop
  * Replaces decompress_audio (fractal.py:1378-1473).  recon values are bit-exact with the reference.
