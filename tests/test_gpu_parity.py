@@ -323,3 +323,17 @@ def test_weighted_energy_is_numpy_f32_sum(n):
     call("fwav_weighted_energy", t.data_ptr(), n, out.data_ptr(), ws.data_ptr(), wn,
          torch.cuda.current_stream().cuda_stream)
     assert bit_equal(out.cpu().numpy(), np.array([np.sum(x ** 2)], np.float32))
+
+
+def test_gather_rows_diagnostic_runs():
+    """fwav_debug_gather_rows (the bench's random-row ceiling for the affine solve) runs on every supported row width
+    and rejects unsupported ones."""
+    from fwav._lib import FwavError
+    st = torch.cuda.current_stream().cuda_stream
+    sink = torch.zeros(1, dtype=torch.float32, device=dev())
+    for rs in (4, 8, 16):
+        tab = torch.rand(100_003 * rs, dtype=torch.float32, device=dev())
+        call("fwav_debug_gather_rows", tab.data_ptr(), 100_003, rs, 1 << 18, sink.data_ptr(), st)
+    torch.cuda.synchronize()
+    with pytest.raises(FwavError):
+        call("fwav_debug_gather_rows", tab.data_ptr(), 100_003, 5, 16, sink.data_ptr(), st)
