@@ -26,15 +26,37 @@ __device__ __forceinline__ int64_t reflect_idx(int64_t p, int64_t n) {
 constexpr int kFramesPerBlock = 1024;
 constexpr int kSignalThreads = 256;
 
-// smoothed energy of frame i; mirrors numpy correlate 'same' with a symmetric kernel (oracle smooth5).
+// Smoothed energy of frame i: np.convolve(e, ones(w, f32)/w, 'same') (fractal.py:893-895) as numpy evaluates it
+// (measured against np.convolve on wide-range random energies; oracle smooth5):
+//   nf ≥ w: window [i − w/2, i − w/2 + w) ∩ [0, nf).  A full window is numpy's small_correlate: f32 products added in
+//           f32 in e order.  A partial window (the first w/2 and last w − w/2 − 1 frames) is the dtype dot (OpenBLAS
+//           sdot): f32 products accumulated in f64 in e order, then rounded.
+//   nf < w: numpy swaps the operands (the kernel correlated with reversed e); frame i covers the e indices j with
+//           0 ≤ t − j ≤ w − 1, t = i + (nf − 1)/2, taken in reversed order: f32 when all nf overlap, else the f64 dot.
 __device__ __forceinline__ float smooth_at(const float* e, int64_t nf, int64_t i, int w, float k) {
-  const int left = w / 2;
-  int64_t lo = i - left, hi = i - left + w;  // window [lo, hi)
-  if (lo < 0) lo = 0;
-  if (hi > nf) hi = nf;
-  float s = 0.0f;
-  for (int64_t j = lo; j < hi; ++j) s = s + e[j] * k;
-  return s;
+  int64_t lo, hi;  // inclusive e index range
+  bool rev;
+  if (nf >= w) {
+    lo = i - w / 2;
+    hi = lo + w - 1;
+    rev = false;
+  } else {
+    hi = i + (nf - 1) / 2;
+    lo = hi - (w - 1);
+    rev = true;
+  }
+  const bool full = rev ? (lo <= 0 && hi >= nf - 1) : (lo >= 0 && hi <= nf - 1);
+  lo = lo < 0 ? 0 : lo;
+  hi = hi > nf - 1 ? nf - 1 : hi;
+  const int64_t cnt = hi - lo + 1;
+  if (full) {
+    float s = 0.0f;
+    for (int64_t t = 0; t < cnt; ++t) s = s + e[rev ? hi - t : lo + t] * k;
+    return s;
+  }
+  double d = 0.0;
+  for (int64_t t = 0; t < cnt; ++t) d += (double)(e[rev ? hi - t : lo + t] * k);
+  return (float)d;
 }
 
 __global__ void k_frame_energy(const float* __restrict__ sig, int64_t n, int frame, int64_t nf,
@@ -350,8 +372,8 @@ int fwav_voiced_ranges(const float* sig, int64_t n, int rs, int frame, int smoot
   FWAV_CHECK_ARG(nr == cdiv(n, rs), FWAV_ERR_SHAPE, "fwav_voiced_ranges: nr != ceil(n/rs)");
   FWAV_CHECK_ARG(frame <= kMaxPairwise, FWAV_ERR_SHAPE, "fwav_voiced_ranges: frame > %d", kMaxPairwise);
   const int64_t nf = cdiv(n, frame);
-  FWAV_CHECK_ARG(smooth_window >= 1 && smooth_window <= 11 && nf >= smooth_window, FWAV_ERR_SHAPE,
-                 "fwav_voiced_ranges: need 1 <= smooth_window <= 11 and n_frames >= smooth_window");
+  FWAV_CHECK_ARG(smooth_window >= 1 && smooth_window <= 11, FWAV_ERR_SHAPE,
+                 "fwav_voiced_ranges: need 1 <= smooth_window <= 11");
   FWAV_CHECK_ARG(ws_bytes >= fwav_voiced_workspace_size(n, frame), FWAV_ERR_WORKSPACE,
                  "fwav_voiced_ranges: workspace too small");
   hipStream_t st = (hipStream_t)stream;
@@ -376,6 +398,22 @@ int fwav_voiced_ranges(const float* sig, int64_t n, int rs, int frame, int smoot
 }
 
 size_t fwav_weighted_energy_workspace_size(int64_t n) { return (size_t)(cdiv(n > 0 ? n : 1, kNpBuf) * 4 + 64); }
+
+__global__ void k_smooth_debug(const float* __restrict__ e, int64_t nf, int w, float k, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nf) out[i] = smooth_at(e, nf, i, w, k);
+}
+
+// Diagnostic (tests): the smoothed frame energies of fwav_voiced_ranges, out[i] for i < nf.
+int fwav_debug_smooth(const float* energy, int64_t nf, int smooth_window, float* out, void* stream) {
+  FWAV_CHECK_ARG(energy && out && nf >= 0 && smooth_window >= 1 && smooth_window <= 11, FWAV_ERR_ARG,
+                 "fwav_debug_smooth: bad args");
+  if (nf == 0) return FWAV_OK;
+  k_smooth_debug<<<cdiv(nf, kSignalThreads), kSignalThreads, 0, (hipStream_t)stream>>>(
+      energy, nf, smooth_window, 1.0f / (float)smooth_window, out);
+  FWAV_LAUNCH_CHECK("fwav_debug_smooth");
+  return FWAV_OK;
+}
 
 // np.sum(ranges[0:n] ** 2) in float32, bit-exact (see k_energy_buffers); the result lands in sum[0].
 int fwav_weighted_energy(const float* ranges, int64_t n, float* sum, void* workspace, size_t ws_bytes, void* stream) {

@@ -25,6 +25,7 @@ SIGNATURES = {
     "fwav_stream_sync": (I32, [P]),
     "fwav_voiced_workspace_size": (SZ, [I64, I32]),
     "fwav_voiced_ranges": (I32, [P, I64, I32, I32, I32, F32, F32, P, I64, P, P, SZ, P]),
+    "fwav_debug_smooth": (I32, [P, I64, I32, P, P]),
     "fwav_weighted_energy_workspace_size": (SZ, [I64]),
     "fwav_weighted_energy": (I32, [P, I64, P, P, SZ, P]),
     "fwav_prune": (I32, [P, I64, I64, I32, F32, I32, P, I64, I32, P, P, P, P, P]),

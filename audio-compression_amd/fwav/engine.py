@@ -181,11 +181,6 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     nf = -(-n // frame)
     nr = -(-n // rs)
     nd = n_domains_for(n, tile_size, step)
-    if nf < 5:
-        # every such input is shorter than the tile for tile >= 40 → the reference's empty result
-        if n < tile_size and tile_size >= 40:
-            return _empty(n, rs, tile_size, step, energy_thresh, k)
-        raise NotImplementedError("inputs shorter than 5 voiced-detection frames need tile_size >= 40")
     thr32 = F32(energy_thresh)
     lo32 = F32(energy_thresh * 0.5)
     if k > size_call("fwav_topk_max_k"):

@@ -53,6 +53,9 @@ int fwav_voiced_ranges(const float* sig, int64_t n, int range_size, int frame, i
  * ranges must be 16-B aligned. */
 size_t fwav_weighted_energy_workspace_size(int64_t n);
 int fwav_weighted_energy(const float* ranges, int64_t n, float* sum, void* workspace, size_t ws_bytes, void* stream);
+/* Diagnostic (tests): out[i] = the smoothed energy of frame i (i < nf) exactly as fwav_voiced_ranges computes it —
+ * np.convolve(energy, ones(w)/w, 'same')[:nf] in numpy's own arithmetic (nf < w included). */
+int fwav_debug_smooth(const float* energy, int64_t nf, int smooth_window, float* out, void* stream);
 
 /* ------------------------------------------------------------------- domain pool + embeddings
  * Replaces build_domains_memmap (fractal.py:285-334) and build_domain_embeddings → multi_head_embedding →

@@ -106,39 +106,50 @@ def frame_energies(signal: np.ndarray, frame_size: int) -> np.ndarray:
 
 
 def smooth5(e: np.ndarray, smooth_window: int = 5) -> np.ndarray:
-    """``np.convolve(e, ones(w,f32)/w, 'same')`` (fractal.py:893-895).  numpy's correlate uses
-    ``small_correlate`` (sequential float32 ``s = 0; s += d[i+j]*k``) for fully-overlapping outputs and the
-    dtype dot (BLAS sdot tail loop: sequential) for the partial ones at both ends."""
+    """``np.convolve(e, ones(w,f32)/w, 'same')`` (fractal.py:893-895) as numpy evaluates it, measured against
+    np.convolve on wide-range random energies (tests/test_oracle_golden.py::test_smooth_matches_numpy):
+      n ≥ w: output i covers e[i − w//2 : i − w//2 + w] ∩ [0, n).  A full window is numpy's small_correlate: f32
+             products added in f32, in e order.  A partial window (the first w//2 and last w − w//2 − 1 outputs) is
+             the dtype dot (OpenBLAS sdot): f32 products accumulated in float64 in e order, then rounded.
+      n < w: numpy swaps the operands (correlate of the kernel with reversed e) and returns w outputs; output j covers
+             the e indices i with 0 ≤ t − i ≤ w − 1, t = j + (n − 1)//2.  A full overlap (all n) is f32 in reversed e
+             order, a partial one the float64-accumulated dot in reversed e order."""
     w = smooth_window
     k = F32(1.0) / F32(w)  # np.ones(w, f32) / w  → float32
+    e = np.asarray(e, F32)
     n = len(e)
-    if n < w:  # np.convolve swaps operands when the kernel is longer; edge-only case
-        k_arr = np.full(w, k, F32)
-        return np.convolve(e.astype(F32), k_arr, mode="same").astype(F32)
+
+    def f32_seq(idx):
+        s = F32(0.0)
+        for i in idx:
+            s = F32(s + F32(e[i] * k))
+        return s
+
+    def f64_dot(idx):
+        s = 0.0
+        for i in idx:
+            s += float(F32(e[i] * k))
+        return F32(s)
+
+    if n < w:
+        out = np.empty(w, F32)
+        off = (n - 1) // 2
+        for j in range(w):
+            t = j + off
+            idx = [i for i in range(n - 1, -1, -1) if 0 <= t - i <= w - 1]
+            out[j] = f32_seq(idx) if len(idx) == n else f64_dot(idx)
+        return out
     left = w // 2
     out = np.empty(n, F32)
-    # partial windows at the left edge: output i uses e[0 : i + w - left]
-    for i in range(left):
-        m = i + w - left
-        s = F32(0.0)
-        for j in range(m):
-            s = F32(s + F32(e[j] * k))
-        out[i] = s
-    # full windows
+    # full windows, vectorised (same f32 order as the scalar loop)
     mid = n - w + 1
-    s = np.zeros(mid, F32)
+    acc = np.zeros(mid, F32)
     for j in range(w):
-        s = s + e[j:j + mid] * k
-    out[left:left + mid] = s
-    # partial windows at the right edge
-    right = w - left - 1
-    for t in range(right):
-        i = left + mid + t
-        start = i - left
-        s = F32(0.0)
-        for j in range(start, n):
-            s = F32(s + F32(e[j] * k))
-        out[i] = s
+        acc = acc + e[j:j + mid] * k
+    out[left:left + mid] = acc
+    for i in list(range(left)) + list(range(left + mid, n)):
+        lo, hi = max(0, i - left), min(n, i - left + w)
+        out[i] = f64_dot(range(lo, hi))
     return out
 
 

@@ -171,6 +171,8 @@ def main():
         "speech4096": (synth.speech_like(2.0, 44100, seed=1, floor=False), 44100, 4, 4096, 1e-4, (64,), False),
         # ragged length (reflect pad of the last range) and an odd tile, K larger than the pool
         "ragged": (synth.noise(0.05, 44100, seed=3)[:2203], 44100, 4, 1000, 1e-4, (16, 2000), True),
+        # fewer than 5 voiced-detection frames (30 samples, frame 8): np.convolve swaps its operands
+        "tiny": (synth.noise(30 / 8000, 8000, seed=9), 8000, 4, 16, 1e-4, (8,), True),
     }
     only = sys.argv[1:]
     for name, (sig, fr, sw, tile, thr, Ks, wf) in cases.items():

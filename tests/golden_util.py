@@ -5,7 +5,7 @@ import os
 import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ["tone", "sweep", "noise2048", "noise4096", "speech4096", "ragged"]
+CASES = ["tone", "sweep", "noise2048", "noise4096", "speech4096", "ragged", "tiny"]
 
 
 def load(case):
@@ -57,7 +57,8 @@ def match_agreement(idx, sym, err, g, K, cand=None, gap=1e-5, rel=1e-5):
 #: the floors the parity tests hold; the remaining mismatches are equal fits (identical tiles) or exact-tie
 #: candidate sets.
 MATCH_FLOOR = {("tone", 32): 0.20, ("sweep", 32): 0.999, ("sweep", 64): 1.0, ("noise2048", 64): 1.0,
-               ("noise4096", 64): 1.0, ("speech4096", 64): 0.993, ("ragged", 16): 1.0, ("ragged", 2000): 1.0}
+               ("noise4096", 64): 1.0, ("speech4096", 64): 0.993, ("ragged", 16): 1.0, ("ragged", 2000): 1.0,
+               ("tiny", 8): 1.0}
 
 #: scores are bit-identical to the reference's (sgemv order), so candidate sets may differ only where the golden K-th
 #: and (K+1)-th scores are exactly equal (numpy's introselect then chooses among the tied domains)

@@ -337,3 +337,20 @@ def test_gather_rows_diagnostic_runs():
     torch.cuda.synchronize()
     with pytest.raises(FwavError):
         call("fwav_debug_gather_rows", tab.data_ptr(), 100_003, 5, 16, sink.data_ptr(), st)
+
+
+@pytest.mark.parametrize("w", [5, 3, 7])
+def test_smoothing_equals_numpy_convolve(w):
+    """fwav_voiced_ranges' moving average (fwav_debug_smooth exposes it) equals np.convolve(e, ones(w)/w, 'same')[:nf]
+    bit-for-bit on energies spanning many decades — full windows in f32, edge windows as numpy's f64-accumulated dot,
+    and fewer frames than taps (numpy swaps the operands)."""
+    rng = np.random.default_rng(w)
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(200):
+        nf = int(rng.integers(1, 40))
+        e = (rng.random(nf) * rng.choice([1e-5, 1e-2, 1.0, 1e3], nf)).astype(np.float32)
+        ref = np.convolve(e, np.full(w, np.float32(1) / np.float32(w), np.float32), mode="same")[:nf]
+        et = td(e)
+        out = torch.empty(nf, dtype=torch.float32, device=dev())
+        call("fwav_debug_smooth", et.data_ptr(), nf, w, out.data_ptr(), st)
+        assert bit_equal(out.cpu().numpy(), ref), (w, nf)

@@ -110,3 +110,17 @@ def test_embedding_heads_at_most_unit_norm(case):
     e = g["emb"].astype(np.float64)
     for head in (e[:, :8], e[:, 8:]):
         assert np.sqrt((head ** 2).sum(1)).max() <= 1 + 1e-6
+
+
+def test_smooth_matches_numpy_convolve():
+    """The voiced detection's moving average is np.convolve(e, ones(5)/5, 'same') (fractal.py:893-895); the oracle's
+    restatement (and the device kernel that mirrors it) must equal numpy bit-for-bit on energies spanning many decades,
+    where the order and precision of each window's sum matter — including fewer frames than taps, where numpy swaps
+    the operands."""
+    rng = np.random.default_rng(11)
+    for w in (5, 3, 7):
+        for _ in range(600):
+            n = int(rng.integers(1, 40))
+            e = (rng.random(n) * rng.choice([1e-5, 1e-2, 1.0, 1e3], n)).astype(np.float32)
+            ref = np.convolve(e, np.full(w, np.float32(1) / np.float32(w), np.float32), mode="same")
+            assert np.array_equal(O.smooth5(e, w).view(np.uint32), ref.view(np.uint32)), (w, n)
