@@ -3,7 +3,9 @@ searches the odd ones with a seed from their neighbours' results: query q scores
 around q − left) of its left neighbour's top K and the mirrored shifts of its right neighbour's, and the K-th best
 of those distinct domains (exact f32, minus 2δ) is a valid band limit.  Times A and B with an -DFWAV_TOPK_EXTSEED
 build (the seeds come from torch here; a device kernel would compute them) and checks that A ∪ B equals the
-one-phase result.  usage: [AB_NQ=...] python tools/phase_ab.py tools/ab/libfwav_ext.so [shifts]"""
+one-phase result.  usage: [AB_NQ=...] python tools/phase_ab.py tools/ab/libfwav_ext.so [shifts]
+Caution: the AB_NQ=41344 run (table pieces + external seeds, a combination the product never launches) ended in a
+memory fault inside a later torch gather; the cause was not found, so do not rerun that case unchanged."""
 import ctypes as C
 import os
 import sys
