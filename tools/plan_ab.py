@@ -29,6 +29,8 @@ st = torch.cuda.current_stream().cuda_stream
 call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
      emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
 nq = int(os.environ.get("AB_NQ", nr))
+if os.environ.get("GEOM"):  # first-pass geometry override: 0 = base, 1 = wide
+    call("fwav_debug_topk_geometry", int(os.environ["GEOM"]))
 active = torch.arange(nq, dtype=torch.int32, device="cuda")
 n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
 ref = None

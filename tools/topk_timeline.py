@@ -63,3 +63,7 @@ order = np.argsort(-(e - s))[:12]
 print("longest workgroups:")
 for i in order:
     print(f"  {ids[i]:5d} {s[i] / 1000:6.2f} {e[i] / 1000:6.2f} {(e[i] - s[i]) / 1000:6.2f}")
+# duration of the workgroups that start with the launch (first round, all in the same phase) vs the later ones
+first = s < 50.0
+print(f"first-round workgroups {int(first.sum())}: median duration {np.median((e - s)[first]) / 1000:.2f} ms; "
+      f"later {int((~first).sum())}: median {np.median((e - s)[~first]) / 1000:.2f} ms")
