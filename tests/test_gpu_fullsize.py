@@ -9,6 +9,8 @@ search (the oracle's scalar top-K would take hours at these sizes):
 * cfg4 (60 min @ 48 kHz, tile 2048: 86,398,977 domains — a 2.76 GB fp16 table, so table offsets pass 2^31): pool and
   embeddings at the end of the table, and a 2,048-range shard searched against the whole table (top-K property,
   affine bit-exact).
+* cfg2 rank shares (the strong-scaling bench's per-rank work at 2 / 4 / 8 ranks): every candidate row of the
+  default work plan (all blocks in table pieces) equals the all-f32 kernel's.
 """
 import numpy as np
 import pytest
@@ -171,3 +173,19 @@ def test_cfg4_table_end_and_shard_search():
     a = O.affine(ranges, cand, pool.cpu().numpy())
     for t, b in zip((res.idx, res.s, res.o, res.sym, res.err), a):
         assert np.array_equal(t.cpu().numpy().view(np.uint8), np.asarray(b).view(np.uint8))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_cfg2_rank_share_equals_f32(world):
+    """One rank's share of the full cfg2 search (the strong-scaling bench's per-rank work): its default work plan
+    splits every query block into table pieces merged by k_merge_pieces (pieces share their band limits), so this
+    is the product path at its real piece counts — every candidate row must equal the all-f32 kernel's."""
+    sig, _, _ = synth.make_config_signal("cfg2")
+    nr = -(-sig.size // 8)
+    lo, hi = (world - 1) * nr // world, nr  # the last rank's block (a shard not starting at 0)
+    res = engine.compress_device(torch.from_numpy(sig).to(dev()), 2048, K, shard=(lo, hi), keep_intermediates=True)
+    torch.cuda.synchronize()
+    cand = res.cand.view(-1, K).cpu().numpy()
+    assert cand.shape[0] == hi - lo and (cand >= 0).all() and (cand < res.n_domains).all()
+    ref = f32_search(res, np.arange(hi - lo), K)
+    assert np.array_equal(cand, ref)
