@@ -342,17 +342,6 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_ABL
 #define FWAV_TOPK_ABL 0
 #endif
-// RING: no workgroup barrier in the stream.  The chunk slots form a ring of 8 / G group slots with LDS counters:
-// a wave that finds the next group's slot free (every wave has left the group that occupied it) claims the group
-// and issues its whole DMA, then publishes it as landed once its own vmcnt drains; a wave streams group g as soon
-// as g is landed.  Waves may drift apart by up to (8 / G − 1) groups, so one wave's window replay no longer holds
-// the other seven at the next barrier.
-#ifndef FWAV_TOPK_RING
-#define FWAV_TOPK_RING 0
-#endif
-// STAGGER: 1 = the second half of the waves takes each group's chunks in rotated order, 2 = every wave of a SIMD
-// pair starts on a different chunk.  Neutral in same-box A/B (21.73 / 21.76 / 22.00 ms for 0 / 1 / 2); a static
-// s_setprio for the second half was slower (+3 %).
 // Exact mode (overflow relaunch) compacts every FWAV_TOPK_EXGROW appends, so its K-th exact key — the store filter —
 // and band limit rise sooner (cfg3 at δ = 2.5e-3: 32 / 64 / 96 / 128 / full buffer 859 / 861 / 870 / 887 / 898 ms;
 // at δ = 2.0e-3: 16 / 24 / 32 / 64 / 128 → 690 / 702 / 695–704 / 711–725 / 727 ms)
@@ -362,9 +351,6 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 // Exact-mode occupancy (waves per SIMD): 2 avoids its register spills but halves the workgroups per CU (856 vs 785 ms)
 #ifndef FWAV_TOPK_EXWPE
 #define FWAV_TOPK_EXWPE 4
-#endif
-#ifndef FWAV_TOPK_STAGGER
-#define FWAV_TOPK_STAGGER 0
 #endif
 constexpr int kGroup = FWAV_TOPK_G;     // chunks per barrier
 constexpr int k16Waves = FWAV_TOPK_W;   // waves per workgroup
@@ -1011,19 +997,17 @@ __device__ __forceinline__ float seed_limit(const _Float16* __restrict__ emb16, 
 // 3 tiles ahead and each MFMA is issued one tile before its fold, across chunk boundaries (a per-chunk loop waits
 // on its first ds_reads and on its last MFMA at every chunk — half the wave time was parked in those waits).
 // With QS query sets per wave each fragment read feeds QS MFMAs (set s: B operand b[s]).  Tile t of a chunk
-// folds into max chain t & 3 of its set; at each chunk end every chain takes one ballot and a firing chunk is
-// recorded in its set's row as (chunk << 4 | chain mask).
+// folds into max chain t % kChains of its set (8 chains: one per tile); at each chunk end one ballot tests the
+// chains' maximum, and a firing chunk is recorded in its set's row as (chunk << 8 | chain mask).
 // MODE (timing ablations, STATS builds only): 1 = fold but no ballots/records, 2 = MFMA with a 2-output fold
 // (one v_max3 per tile instead of 8; results kept alive through `sink`).
-// ROT: the group's chunks are taken in rotated order (chunk (k + ROT) mod NC at step k) — a stagger between the
-// two halves of the workgroup, which otherwise reach their MFMA and fold phases in lockstep.
-template <int NC, int QS, int MODE = 0, int ROT = 0>
+template <int NC, int QS, int MODE = 0>
 __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, const half8 (&b)[QS],
                                              const int (&thi)[QS], int cbase, uint32_t (*fired)[kFifo],
                                              int (&nfired)[QS], int lane, int* sink = nullptr) {
   constexpr int NT = 8 * NC;
   constexpr int kChunkHalfs = 512 * 8;  // one 8 KB chunk slot
-  auto chunk_of = [](int i) { return ((i >> 3) + ROT) % NC; };
+  auto chunk_of = [](int i) { return i >> 3; };
   auto rd = [&](int i) {
     return *reinterpret_cast<const half8*>(lda0 + chunk_of(i) * kChunkHalfs + (i & 7) * 256);
   };
@@ -1101,13 +1085,9 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
   // ALL of the kernel's LDS is one __shared__ object: beside a second one, hipcc waits vmcnt(0) for the in-flight
   // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
-  constexpr bool kRing = FWAV_TOPK_RING != 0;
-  constexpr int NGS = kRing ? 8 / G : 2;  // group slots
   struct Lds {
-    u32x4 slots[NGS * G][512];
+    u32x4 slots[2 * G][512];
     Topk16SmemT<NG, STATS> sm;
-    uint32_t ring_landed[NGS];  // RING: waves whose DMA part has landed in the slot (monotonic: W per generation)
-    uint32_t ring_left[NGS];    // RING: waves that have finished reading the slot (monotonic: W per generation)
   };
   __shared__ __attribute__((aligned(16))) Lds lds_all;
   u32x4(*slots)[512] = lds_all.slots;
@@ -1240,7 +1220,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
   // retire the prologue's ordinary loads (query fragments, active list) before the stream, visibly to hipcc
   // (a load still pending at the loop head is waited on, vmcnt(0), inside every chunk iteration)
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  if (!kRing && ngroups > 0) issue_group(0);
+  if (ngroups > 0) issue_group(0);
 
   int sink = 0;     // ablation builds: keeps the MFMA / fold results of dbg 512/1024 alive
   int nfired[QS];  // wave-uniform FIFO tail: chunks recorded in sm.fired[group] so far
@@ -1252,99 +1232,6 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
     nfired[s] = qcnt[s] = kept[s] = 0;
     cur[s] = ReplayCursor{0, 0, 0u};
   }
-  if constexpr (kRing) {
-    // ---------------------------------------------------------------- barrier-free ring (FWAV_TOPK_RING)
-    if (tid < NGS) {
-      lds_all.ring_landed[tid] = 0u;
-      lds_all.ring_left[tid] = 0u;
-    }
-    __syncthreads();  // counters (and the prologue's sm writes) visible to every wave
-    auto ld_acq = [](uint32_t* p) {
-      return (uint32_t)__builtin_amdgcn_readfirstlane(
-          (int)__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-    };
-    // this wave's share of group gg's DMA (the same 8·G / W wave-instructions as the barrier loop)
-    auto issue_part = [&](int64_t gg) {
-#pragma unroll
-      for (int j = 0; j < G; ++j) {
-        int64_t c_ = c0 + gg * G + j;
-        c_ = c_ < c1 ? c_ : c1 - 1;
-        for (int k = wave; k < 8; k += Wact) {
-          const unsigned lds_dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(
-              (__attribute__((address_space(3))) void*)(&slots[(gg % NGS) * G + j][k * 64])));
-          const u32x4* gsrc = src + (int64_t)c_ * 512 + k * 64 + lane;
-          unsigned keep;
-          asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                       : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-        }
-      }
-    };
-    // Groups [pub, iss) have this wave's part issued but not yet counted as landed.  Every wave issues its part of
-    // group c once the slot is free (all W waves have left group c − NGS) and publishes it (ring_landed += 1) after
-    // its own vmcnt drains; group c is readable when ring_landed of its slot reaches W per generation.
-    int64_t iss = 0, pub = 0;
-    auto publish = [&]() {
-      if (pub == iss) return;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
-      for (; pub < iss; ++pub)
-        if (lane == 0)
-          __hip_atomic_fetch_add(&lds_all.ring_landed[pub % NGS], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    auto try_issue = [&](int64_t upto) {
-      upto = upto < ngroups - 1 ? upto : ngroups - 1;
-      while (iss <= upto && ld_acq(&lds_all.ring_left[iss % NGS]) >= (uint32_t)(Wact * (iss / NGS))) issue_part(iss++);
-    };
-    for (int64_t g = 0; g < ngroups; ++g) {
-      u32x4(*half)[512] = slots + (g % NGS) * G;
-      const int64_t cg = c0 + g * G;
-      const int64_t c_end = cg + G < c1 ? cg + G : c1;
-      const bool window_end =
-          (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
-      const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-      try_issue(g + NGS - 1);
-      for (int spins = 0; ld_acq(&lds_all.ring_landed[g % NGS]) < (uint32_t)(Wact * (g / NGS + 1)); ++spins) {
-        publish();  // part of the group may be this wave's own
-        try_issue(g + NGS - 1);
-        __builtin_amdgcn_s_sleep(1);
-        if (spins > (1 << 22)) break;  // never expected: bounded so a logic error cannot hang the GPU
-      }
-      const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-      if (STATS) stat_add(7, t_b1 - t_b0);
-      int thi[QS];
-#pragma unroll
-      for (int s = 0; s < QS; ++s) thi[s] = int_threshold(HL ? thf[s] - kStreamMargin : thf[s]);
-      const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
-      if (c_end - cg == G) {
-#if FWAV_TOPK_STAGGER
-        if (wave >= W / 2)
-          stream_group<G, QS, 0, G / 2>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
-        else
-#endif
-          stream_group<G, QS>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
-      } else {
-        for (int64_t c = cg; c < c_end; ++c)
-          stream_group<1, QS>(lda0 + (c - cg) * 512 * 8, b, thi, c, sm.fired + wave * QS, nfired, lane);
-      }
-      // this wave is done with the slot (its ds_reads were consumed by the MFMAs)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0)
-        __hip_atomic_fetch_add(&lds_all.ring_left[g % NGS], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      publish();
-      const unsigned long long t_c = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-      if (STATS) stat_add(9, t_c - t_b1);
-      if (window_end) {
-#pragma unroll
-        for (int s = 0; s < QS; ++s) {
-          if (nfired[s] > cur[s].head || cur[s].rem != 0u)
-            thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s], qcnt[s], kept[s], cur[s],
-                                             nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s], share);
-        }
-        if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-      }
-    }
-    publish();
-  } else
   for (int g = 0; g < ngroups; ++g) {
     u32x4(*half)[512] = slots + (g & 1) * G;
     const int cg = c0 + g * G;  // first chunk of group g
@@ -1374,22 +1261,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
       else
         stream_group<G, QS, 1>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane, &sink);
     } else if (c_end - cg == G) {
-#if FWAV_TOPK_STAGGER == 2
-      // every wave of a SIMD pair starts the group on a different chunk
-      switch (wave & (G - 1)) {
-        case 0: stream_group<G, QS, 0, 0>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane); break;
-        case 1: stream_group<G, QS, 0, (1 % G)>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane); break;
-        case 2: stream_group<G, QS, 0, (2 % G)>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane); break;
-        default: stream_group<G, QS, 0, (3 % G)>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane); break;
-      }
-#else
-#if FWAV_TOPK_STAGGER
-      if (wave >= W / 2)
-        stream_group<G, QS, 0, G / 2>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
-      else
-#endif
-        stream_group<G, QS>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
-#endif
+      stream_group<G, QS>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane);
     } else {
       for (int c = cg; c < c_end; ++c)
         stream_group<1, QS>(lda0 + (c - cg) * 512 * 8, b, thi, c, sm.fired + wave * QS, nfired, lane);
@@ -1541,12 +1413,13 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   int mb = 0;
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
-    if (u >= nu) break;
-    const bool keep = x[u] != 0ull && (uint32_t)(x[u] >> 32) > L;
-    const uint64_t bm = __ballot(keep);
-    const int pos = mb + __popcll(bm & ((1ull << lane) - 1ull));
-    if (keep && pos < C) sw[pos] = x[u];
-    mb += __popcll(bm);
+    if (u < nu) {  // (no early break: the loop must unroll to keep x[] in registers)
+      const bool keep = x[u] != 0ull && (uint32_t)(x[u] >> 32) > L;
+      const uint64_t bm = __ballot(keep);
+      const int pos = mb + __popcll(bm & ((1ull << lane) - 1ull));
+      if (keep && pos < C) sw[pos] = x[u];
+      mb += __popcll(bm);
+    }
   }
   uint64_t v[E];
 #pragma unroll
