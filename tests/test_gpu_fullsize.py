@@ -189,3 +189,14 @@ def test_cfg2_rank_share_equals_f32(world):
     assert cand.shape[0] == hi - lo and (cand >= 0).all() and (cand < res.n_domains).all()
     ref = f32_search(res, np.arange(hi - lo), K)
     assert np.array_equal(cand, ref)
+
+
+def test_cfg2_whole_search_equals_f32():
+    """The whole cfg2 search (1,292 query blocks on 512 workgroup slots, the tail in table pieces) equals the all-f32
+    kernel on every row."""
+    sig, _, _ = synth.make_config_signal("cfg2")
+    res = engine.compress_device(torch.from_numpy(sig).to(dev()), 2048, K, keep_intermediates=True)
+    torch.cuda.synchronize()
+    cand = res.cand.view(-1, K).cpu().numpy()
+    assert (cand >= 0).all() and (cand < res.n_domains).all()
+    assert np.array_equal(cand, f32_search(res, np.arange(res.n_ranges), K))
