@@ -13,6 +13,16 @@
 //
 // The n_ranges × n_domains score matrix (4.4e11 entries at cfg2) is never materialised.
 //
+// Production path (emb16 != NULL), in file order: the work plan (query blocks, table pieces, query halves);
+// k_sim_topk_f16 — 8 waves × 32 queries per workgroup (16 waves, one per CU, above 8 Mi domains), the fp16 table
+// streamed through LDS by LDS-DMA in groups of 4 chunks, one fp16 MFMA per 32-domain tile and a max-fold per lane
+// (stream_group), fired chunks replayed at window ends into per-query two-ended key buffers with inline compaction
+// (replay_window / append_tile / compact16_s16), band limits seeded from each query's own domain window
+// (seed_limit) and shared between the table pieces of a query (atomicMax), an exact f32 final pass in the
+// reference's sgemv order (compact16) or a band hand-off to k_merge_pieces (piece_band); then the device-side
+// overflow lists relaunch the same kernel in the narrower HL and exact modes.  Measurements behind every constant:
+// DESIGN.md §3.1.
+//
 // k_sim_topk_f32 (emb16 == NULL; tests and a reference for the production kernel below): workgroup = 4 waves × 32
 // queries; each 256-domain chunk is staged row-major in LDS and every lane scores its query against 16 domain rows
 // of each 32-domain tile with sgemv16 (VALU), keeps a running threshold θ (one register per lane), and appends
