@@ -1761,6 +1761,31 @@ int fwav_debug_topk_geometry(int wide) {
   return FWAV_OK;
 }
 
+// Host-side check of the work plan (no device needed): for every item of the plan of n queries (rt, pieces as in
+// fwav_debug_topk_plan; wide: the 16-wave geometry) and every query slot its workgroup runs, count[position] += 1.
+// A query of a whole-table block or a query half must be counted once, one of a block split into P table pieces P
+// times.  *items = the launch's grid.
+int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t* count, int64_t* items) {
+  FWAV_CHECK_ARG(n >= 0 && count && items && (pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces)), FWAV_ERR_ARG,
+                 "fwav_debug_topk_plan_cover: bad args");
+  const int W = wide ? kWideW : k16Waves, qb = 32 * W * k16Sets;
+  const TopkPlan pl = make_plan(n, rt, pieces, qb);
+  *items = pl.items();
+  for (int64_t it = 0; it < pl.items(); ++it) {
+    int64_t block;
+    int piece, np, qhalf;
+    plan_item(pl, it, block, piece, np, qhalf);
+    if (block >= pl.nb) continue;
+    const int wact = qhalf < 0 ? W : W / 2;
+    const int qslot0 = qhalf > 0 ? (W / 2) * k16Sets * 32 : 0;
+    for (int ql = 0; ql < wact * k16Sets * 32; ++ql) {
+      const int64_t qi = slot_query(block, qslot0 + ql, pl.nb, qb);
+      if (qi < n) ++count[qi];
+    }
+  }
+  return FWAV_OK;
+}
+
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.
 int fwav_debug_topk_plan(int rt, int pieces) {

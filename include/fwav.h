@@ -108,6 +108,9 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, 
  * ranges, or with pieces == -1 into two query halves (rt < 0 restores the default policy).  Every plan returns the
  * same candidates.  Re-query fwav_sim_topk_workspace_size afterwards. */
 int fwav_debug_topk_plan(int rt, int pieces);
+/* Host-side check of a work plan (no device): count[position] += 1 for every query slot of every item of the plan of
+ * n queries (whole blocks and query halves cover a query once, a block in P table pieces P times); *items = grid. */
+int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t* count, int64_t* items);
 /* Diagnostic override of the fp16 search's first-pass mode: 0 = fp16 band (overflowing queries relaunched with the
  * hi/lo band, then exact keys), 1 = hi/lo band (then exact keys), −1 = by table size (the default: hi/lo above 4 Mi
  * domains).  Every mode returns the same candidates. */

@@ -89,3 +89,26 @@ def test_workspace_sizes(lib):
     big = size_call("fwav_sim_topk_workspace_size", 330750, 1321977, 1000)
     assert 1321977 * 4 <= big <= (1 << 30)
     assert size_call("fwav_sim_topk_workspace_size", 10, 1000, 1000) == 10 * 1000 * 4
+
+
+@pytest.mark.parametrize("wide", [0, 1])
+@pytest.mark.parametrize("n,rt,pieces", [(330750, 0, 1), (330750, 24, 4), (41344, 1 << 20, 3), (165375, 134, 4),
+                                         (1000, 1 << 20, 8), (70000, 7, -1), (33, 3, 2), (256 * 5, 2, 5)])
+def test_work_plan_covers_every_query(lib, n, rt, pieces, wide):
+    """Host-side: the fp16 search's work plan (query blocks, INTERLEAVEd query groups, table pieces, query halves)
+    runs every active query exactly once per table piece of its block and nothing past the list."""
+    count = np.zeros(n, np.int32)
+    items = ctypes.c_int64()
+    lib.call("fwav_debug_topk_plan_cover", n, rt, pieces, wide, count.ctypes.data, ctypes.addressof(items))
+    qb = 32 * (16 if wide else 8)
+    nb = -(-n // qb)
+    P = 1 if pieces == 1 else (2 if pieces == -1 else pieces)
+    R = 0 if P == 1 else min(nb, rt)
+    assert items.value == (nb - R) + R * P
+    # queries of the split blocks (the last R blocks under the interleaved mapping) are counted P times (halves: once)
+    expect = np.ones(n, np.int32)
+    if pieces > 1 and R:
+        g = np.arange(n) // 32
+        split = (g % nb) >= nb - R
+        expect[split] = pieces
+    assert np.array_equal(count, expect)
