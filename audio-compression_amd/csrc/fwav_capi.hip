@@ -18,7 +18,13 @@ extern "C" {
 
 const char* fwav_last_error(void) { return fwav::g_err; }
 
-int fwav_abi_version(void) { return 2; }
+int fwav_abi_version(void) { return 3; }
+
+#ifndef FWAV_SOURCE_DIGEST
+#define FWAV_SOURCE_DIGEST "unknown"
+#endif
+// SHA-256 of the sources + compiler flags (fwav/_digest.py), passed in by __graft_entry__.build.
+const char* fwav_build_digest(void) { return FWAV_SOURCE_DIGEST; }
 
 // Block until all work queued on `stream` is done; reports asynchronous kernel faults.
 int fwav_stream_sync(void* stream) {

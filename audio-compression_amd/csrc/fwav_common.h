@@ -108,17 +108,66 @@ __device__ __forceinline__ auto pw_sum_n(const F& f) -> decltype(f(0)) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// The reference's f32 similarity score, emb_dom @ q (fractal.py:537), in the order its BLAS evaluates it: numpy's
-// sgemv on the (n_domains, 16) table goes to OpenBLAS sgemv_t, whose 4-column microkernel (Haswell/Zen/SkylakeX)
-// accumulates the 16 products in 8 fma lanes, l_j = fma(d[j+8], q[j+8], d[j]·q[j]), then reduces 256 → 128 bits
-// and adds horizontally: ((l0 + l4) + (l1 + l5)) + ((l2 + l6) + (l3 + l7)).  Measured bit-exact against
-// numpy (OpenBLAS 0.3.29) on every golden table except its last n_domains mod 4 columns, which OpenBLAS scores
-// with a different kernel.  D(k) and Q(k) return the k-th element of the domain row and of the query.
+// The reference's f32 similarity scores, emb_dom @ q (fractal.py:537), in the order its BLAS evaluates them: numpy's
+// sgemv on the (n_domains, 16) table goes to OpenBLAS 0.3.29 sgemv_t (Haswell/Zen/SkylakeX kernels), which scores
+// a column (domain) with one of three kernels (oracle/fractal_oracle.py sgemv_col_kind / sgemv_scores, pinned
+// against numpy on every column for 1, 3, 5, 7 and 8 threads):
+//   kind 0, the 4-column microkernel: 8 fma lanes l_j = fma(d[j+8], q[j+8], 0 + d[j]·q[j]), then 256 → 128 bits and
+//           two horizontal adds: ((l0 + l4) + (l1 + l5)) + ((l2 + l6) + (l3 + l7));
+//   kind 1, the 4x2 tail kernel (SSE): l_j = (((0 + p_j) + p_{j+4}) + p_{j+8}) + p_{j+12} of the rounded products
+//           p_k = d[k]·q[k], then (l0 + l1) + (l2 + l3);
+//   kind 2, the 4x1 tail kernel: l_j = (0 + p_j) + p_{j+8} (8 lanes), then ((l0 + l4) + (l1 + l5)) + ((l2 + l6) + …).
+// Which kernel scores domain d depends on how gemv_thread.c splits the nd columns over OpenBLAS's T threads (T = 1
+// while 16·nd < 460,800): widths ceil(rest / threads left), i.e. the first nd mod T chunks one column wider, and each
+// chunk's last (width mod 4) columns go to the tail kernels (2 → 4x2, 1 → 4x1, 3 → 4x2 then 4x1).  D(k) and Q(k)
+// return the k-th element of the domain row and of the query.
+struct SgemvSplit {
+  uint32_t q, r;  // chunk width q; the first r chunks are q + 1 wide
+};
+__host__ inline SgemvSplit make_sgemv_split(int64_t nd, int threads) {
+  const int64_t T = (16 * nd < 460800 || threads < 1) ? 1 : threads;
+  return SgemvSplit{(uint32_t)(nd / T), (uint32_t)(nd % T)};
+}
+__device__ __forceinline__ int sgemv_kind(uint32_t d, const SgemvSplit& sp) {
+  const uint32_t big = sp.r * (sp.q + 1);
+  uint32_t w, start;
+  if (d < big) {
+    w = sp.q + 1;
+    start = d - d % w;
+  } else {
+    w = sp.q;
+    start = d - (d - big) % w;
+  }
+  const uint32_t pos = d - start, t = w & 3u;
+  if (pos < w - t) return 0;
+  return ((t & 2u) && pos < w - t + 2) ? 1 : 2;
+}
+// First column of d's thread chunk; [d0, d1] is all kind 0 iff d1 is kind 0 and d0 ≥ sgemv_chunk_start(d1)
+// (each chunk's kind-0 columns are a prefix of it).
+__device__ __forceinline__ uint32_t sgemv_chunk_start(uint32_t d, const SgemvSplit& sp) {
+  const uint32_t big = sp.r * (sp.q + 1);
+  return d < big ? d - d % (sp.q + 1) : d - (d - big) % sp.q;
+}
 template <class D, class Q>
-__device__ __forceinline__ float sgemv16(const D& d, const Q& q) {
+__device__ __forceinline__ float sgemv16(const D& d, const Q& q, int kind = 0) {
+  if (kind == 0) {
+    float l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) l[j] = __builtin_fmaf(d(j + 8), q(j + 8), 0.0f + d(j) * q(j));
+    return ((l[0] + l[4]) + (l[1] + l[5])) + ((l[2] + l[6]) + (l[3] + l[7]));
+  }
+  float p[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) p[k] = d(k) * q(k);
+  if (kind == 1) {
+    float l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) l[j] = (((0.0f + p[j]) + p[j + 4]) + p[j + 8]) + p[j + 12];
+    return (l[0] + l[1]) + (l[2] + l[3]);
+  }
   float l[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) l[j] = __builtin_fmaf(d(j + 8), q(j + 8), d(j) * q(j));
+  for (int j = 0; j < 8; ++j) l[j] = (0.0f + p[j]) + p[j + 8];
   return ((l[0] + l[4]) + (l[1] + l[5])) + ((l[2] + l[6]) + (l[3] + l[7]));
 }
 

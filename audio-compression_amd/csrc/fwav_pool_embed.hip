@@ -10,17 +10,22 @@
 // so only ≈ n/step block means are computed instead of nd·rs (8× less work at tile 2048): k_block_means.
 // Otherwise k_domain_pool computes every (d, k) directly.
 //
-// Embedding (per domain, one thread).  The reference runs scipy's pocketfft per row; here the orthonormal
-// DCT-II rows the embedding keeps are constant matrices built on the host in float64 (fwav_embed_tables),
-// with the linspace(1, 2, n) weights folded in, evaluated in f64:
-//   tonal[j]     = f32( Σ_n C[j+1][n]·w[j+1]·x[n] ),  j < min(8, rs−1), zero-padded; ‖·‖ f32, /‖·‖ if > 1e-8
-//   transient[k] = Σ_n C[k][n]·w[n]·f64(x[n] − x[n−1]),  k < min(8, rs); f64 norm; /‖·‖ if > 1e-8; → f32
-// Parity is |Δ| ≤ 1e-6 against the reference goldens (SURVEY Appendix A rule 2).
-// Invariant relied on elsewhere: each head has norm ≤ 1 (normalised, or zero).  The similarity search's fp16 error
-// bound δ (fwav_topk.hip kF16Delta) assumes Σ|q_k d_k| ≤ ‖q‖‖d‖ ≤ 2; a change here that breaks it (e.g. honouring
-// transient_weight) must change δ too.  Checked by tests (test_embedding_heads_at_most_unit_norm, full-size cfg3).
+// Embedding (per domain, one thread), bit-exact with the reference for range sizes 4, 8 and 16 (every config in
+// BASELINE.json and the goldens):
+//   tonal[j]     = f32( f32-DCT(x)[j+1] · w[j+1] ), j < min(8, rs−1), zero-padded to 8; ‖·‖ as np.linalg.norm of a
+//                  1-D float32 vector evaluates it (OpenBLAS sdot: f32 products summed in f64, rounded to f32, f32
+//                  sqrt); / ‖·‖ in f32 if ‖·‖ > f32(1e-8)                                    (fractal.py:178-208)
+//   transient[k] = f64-DCT(f64(x[n] − x[n−1]) · w[n])[k], k < min(8, rs); ‖·‖ as ddot (n < 16: a sequential f64 fma
+//                  chain) then sqrt; / ‖·‖ if > 1e-8; → f32                                  (fractal.py:154-164)
+// with the DCTs scipy's own pocketfft operation sequence in each precision (fwav_dct.h) and w = np.linspace(1, 2, rs)
+// as numpy computes it (i·(1/(rs−1)) + 1, last = 2).  Other range sizes take the f64 matrix DCT (within 1e-6,
+// SURVEY Appendix A rule 2).  fwav_embed_tables packs the matrices and pocketfft's constants for both precisions.
 #include "fwav_common.h"
+#include "fwav_dct.h"
 #include "../../include/fwav.h"
+
+#include <utility>
+#include <vector>
 
 namespace fwav {
 
@@ -74,7 +79,13 @@ __global__ void k_embed(const float* __restrict__ src, int64_t nd, int rs, int64
   const double* td = tab + 8 * n;
   float e[8];
   double t[8];
-  if constexpr (RS > 0) {
+  float tf[8];
+  if constexpr (RS == 4 || RS == 8 || RS == 16) {
+    // exact path: scipy's pocketfft DCTs and numpy's / OpenBLAS's norm orders (see the file header)
+    DctK<float, RS> kf;
+    DctK<double, RS> kd;
+    dct_load(kf, tab + 16 * RS);
+    dct_load(kd, tab + 16 * RS + dct_block(RS));
     float x[RS];
 #pragma unroll
     for (int i = 0; i < RS; ++i) x[i] = xs[i * b];
@@ -82,20 +93,34 @@ __global__ void k_embed(const float* __restrict__ src, int64_t nd, int rs, int64
 #pragma unroll
       for (int i = 0; i < RS; ++i) pool_out[d * RS + i] = x[i];
     }
+    float c[RS];
+#pragma unroll
+    for (int i = 0; i < RS; ++i) c[i] = x[i];
+    dct2_ortho<float, RS>(c, kf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = j < take ? (float)((double)c[j + 1 < RS ? j + 1 : 0] * kd.w[j + 1 < RS ? j + 1 : 0]) : 0.0f;
+    double acc = 0.0;  // sdot: f32 products, f64 sum in index order, f32 result
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = acc + (double)(e[j] * e[j]);
+    const float nrm = sqrtf((float)acc);
+    if (nrm > 1e-8f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = e[j] / nrm;
+    }
+    double dv[RS];
+#pragma unroll
+    for (int i = 0; i < RS; ++i) dv[i] = (double)(i == 0 ? x[0] - x[0] : x[i] - x[i - 1]) * kd.w[i];
+    dct2_ortho<double, RS>(dv, kd);
+    double s2 = 0.0;  // ddot, n < 16: fma chain
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < tk) s2 = __builtin_fma(dv[j < RS ? j : 0], dv[j < RS ? j : 0], s2);
+    const double nrmd = sqrt(s2);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      double acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < RS; ++i) acc += tt[j * RS + i] * (double)x[i];
-      e[j] = j < take ? (float)acc : 0.0f;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = 0.0;
-#pragma unroll
-    for (int i = 0; i < RS; ++i) {
-      const double dd = (double)(i == 0 ? x[0] - x[0] : x[i] - x[i - 1]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) t[j] += td[j * RS + i] * dd;
+      double v = j < tk ? dv[j < RS ? j : 0] : 0.0;
+      if (nrmd > 1e-8) v = v / nrmd;
+      tf[j] = (float)v;
     }
   } else {
     if (pool_out) {
@@ -113,27 +138,21 @@ __global__ void k_embed(const float* __restrict__ src, int64_t nd, int rs, int64
       double dd = (double)(xi - xp);
       for (int j = 0; j < 8; ++j) t[j] += td[j * n + i] * dd;
     }
-  }
-  // tonal: f32 norm (short sdot: sequential), normalise if > 1e-8
-  float s2 = 0.0f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s2 = s2 + e[j] * e[j];
-  float nrm = sqrtf(s2);
-  if (nrm > 1e-8f) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) e[j] = e[j] / nrm;
-  }
-  // transient: f64 norm over the tk kept coefficients
-  double s2d = 0.0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s2d += j < tk ? t[j] * t[j] : 0.0;
-  double nd64 = sqrt(s2d);
-  float tf[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    double v = j < tk ? t[j] : 0.0;
-    if (nd64 > 1e-8) v = v / nd64;
-    tf[j] = (float)v;
+    double acc = 0.0;  // tonal norm in sdot order
+    for (int j = 0; j < 8; ++j) acc = acc + (double)(e[j] * e[j]);
+    const float nrm = sqrtf((float)acc);
+    if (nrm > 1e-8f) {
+      for (int j = 0; j < 8; ++j) e[j] = e[j] / nrm;
+    }
+    double s2d = 0.0;  // transient: ddot fma chain over the tk kept coefficients
+    for (int j = 0; j < 8; ++j)
+      if (j < tk) s2d = __builtin_fma(t[j], t[j], s2d);
+    const double nd64 = sqrt(s2d);
+    for (int j = 0; j < 8; ++j) {
+      double v = j < tk ? t[j] : 0.0;
+      if (nd64 > 1e-8) v = v / nd64;
+      tf[j] = (float)v;
+    }
   }
   // concatenation [tonal 8 | transient tk] then zero pad to 16 (multi_head_embedding :170-175)
   float out[16];
@@ -174,6 +193,79 @@ static void launch_embed(const float* src, int64_t nd, int rs, int64_t a, int64_
   k_embed<RS><<<cdiv(nd, kPoolThreads), kPoolThreads, 0, st>>>(src, nd, rs, a, b, tab, pool_out, emb, emb16);
 }
 
+// pocketfft's sincos_2pibyn<T>(n)[idx] (Thigh = double for float and double): a two-level table of octant-reduced
+// cos/sin in double, entries multiplied in double — reproduced so that the twiddles are pocketfft's own values.
+struct SinCos2PiByN {
+  size_t n, shift, mask;
+  std::vector<std::pair<double, double>> v1, v2;
+  static std::pair<double, double> calc(size_t x, size_t n, double ang) {
+    x <<= 3;
+    if (x < 4 * n) {
+      if (x < 2 * n) {
+        if (x < n) return {std::cos(double(x) * ang), std::sin(double(x) * ang)};
+        return {std::sin(double(2 * n - x) * ang), std::cos(double(2 * n - x) * ang)};
+      }
+      x -= 2 * n;
+      if (x < n) return {-std::sin(double(x) * ang), std::cos(double(x) * ang)};
+      return {-std::cos(double(2 * n - x) * ang), std::sin(double(2 * n - x) * ang)};
+    }
+    x = 8 * n - x;
+    if (x < 2 * n) {
+      if (x < n) return {std::cos(double(x) * ang), -std::sin(double(x) * ang)};
+      return {std::sin(double(2 * n - x) * ang), -std::cos(double(2 * n - x) * ang)};
+    }
+    x -= 2 * n;
+    if (x < n) return {-std::sin(double(x) * ang), -std::cos(double(x) * ang)};
+    return {-std::cos(double(2 * n - x) * ang), -std::sin(double(2 * n - x) * ang)};
+  }
+  explicit SinCos2PiByN(size_t n_) : n(n_) {
+    const long double pi = 3.141592653589793238462643383279502884197L;
+    const double ang = (double)(0.25L * pi / (long double)n);
+    const size_t nval = (n + 2) / 2;
+    shift = 1;
+    while (((size_t)1 << shift) * ((size_t)1 << shift) < nval) ++shift;
+    mask = ((size_t)1 << shift) - 1;
+    v1.resize(mask + 1);
+    v1[0] = {1.0, 0.0};
+    for (size_t i = 1; i < v1.size(); ++i) v1[i] = calc(i, n, ang);
+    v2.resize((nval + mask) / (mask + 1));
+    v2[0] = {1.0, 0.0};
+    for (size_t i = 1; i < v2.size(); ++i) v2[i] = calc(i * (mask + 1), n, ang);
+  }
+  std::pair<double, double> operator[](size_t idx) const {
+    if (2 * idx <= n) {
+      const auto x1 = v1[idx & mask], x2 = v2[idx >> shift];
+      return {x1.first * x2.first - x1.second * x2.second, x1.first * x2.second + x1.second * x2.first};
+    }
+    idx = n - idx;
+    const auto x1 = v1[idx & mask], x2 = v2[idx >> shift];
+    return {x1.first * x2.first - x1.second * x2.second, -(x1.first * x2.second + x1.second * x2.first)};
+  }
+};
+
+// DctK<T, n> constants (T = double if dbl, else float, stored as doubles) exactly as pocketfft / numpy compute them:
+// T_dcst23 twiddle[i] = T(sincos_2pibyn(4n)[i+1].r); the first rfftp factor's twiddles (comp_twiddle); fct =
+// T(1/sqrt(long double(2n))); sqrt2 = T(1.414…L); w = np.linspace(1, 2, n) in double (arange · (1/(n−1)) + 1, last 2).
+void dct_constants(int n, bool dbl, double* out) {
+  auto r = [&](long double v) { return dbl ? (double)v : (double)(float)v; };
+  for (int i = 0; i < 9; ++i) out[n + i] = 0.0;
+  const SinCos2PiByN s4(4 * (size_t)n), s1((size_t)n);
+  for (int i = 0; i < n; ++i) out[i] = r(s4[i + 1].first);
+  if (n == 8) {  // radb2, l1 = 1, ido = 4
+    out[n + 0] = r(s1[1].first);
+    out[n + 1] = r(s1[1].second);
+  } else if (n == 16) {  // radb4, l1 = 1, ido = 4
+    for (int j = 1; j < 4; ++j) {
+      out[n + (j - 1) * 3 + 0] = r(s1[j].first);
+      out[n + (j - 1) * 3 + 1] = r(s1[j].second);
+    }
+  }
+  const double step = 1.0 / (double)(n - 1);
+  for (int i = 0; i < n; ++i) out[n + 9 + i] = i == n - 1 ? 2.0 : (double)i * step + 1.0;
+  out[2 * n + 9] = r(1.0L / std::sqrt((long double)(2 * n)));
+  out[2 * n + 10] = r(1.414213562373095048801688724209698L);
+}
+
 }  // namespace fwav
 
 using namespace fwav;
@@ -182,7 +274,12 @@ extern "C" {
 
 size_t fwav_emb16_elems(int64_t nd) { return (size_t)(2 * ((nd + 255) / 256) * 256 * 16); }
 
-// Host-side f64 tables for fwav_pool_embed: tab[16 * rs] (tonal 8 rows, transient 8 rows).
+// Host-side f64 tables for fwav_pool_embed: tab[fwav_embed_tables_size(rs)] = the matrices (tonal 8 rows, transient 8
+// rows of rs) and, for rs = 4, 8, 16, pocketfft's constants in float32 then float64 (DctK layout, dct_constants).
+size_t fwav_embed_tables_size(int rs) {
+  return (size_t)16 * rs + ((rs == 4 || rs == 8 || rs == 16) ? 2 * (size_t)dct_block(rs) : 0);
+}
+
 int fwav_embed_tables(int rs, double* tab) {
   FWAV_CHECK_ARG(rs >= 1 && rs <= kMaxPairwise && tab, FWAV_ERR_ARG, "fwav_embed_tables: bad args");
   const double pi = 3.14159265358979323846;
@@ -198,6 +295,37 @@ int fwav_embed_tables(int rs, double* tab) {
     for (int i = 0; i < n; ++i) tab[j * n + i] = j < take ? c(j + 1, i) * w(j + 1) : 0.0;
   for (int j = 0; j < 8; ++j)
     for (int i = 0; i < n; ++i) tab[8 * n + j * n + i] = j < tk ? c(j, i) * w(i) : 0.0;
+  if (rs == 4 || rs == 8 || rs == 16) {
+    dct_constants(rs, false, tab + 16 * rs);
+    dct_constants(rs, true, tab + 16 * rs + dct_block(rs));
+  }
+  return FWAV_OK;
+}
+
+// Test hook (host): scipy.fftpack.dct(x, norm='ortho') of n = 4, 8, 16 doubles (dbl = 1) or floats (dbl = 0, passed
+// and returned as doubles) through fwav_dct.h — the code the embedding kernel runs, instantiated on the host.
+int fwav_debug_dct2(int n, int dbl, const double* x, double* out) {
+  FWAV_CHECK_ARG((n == 4 || n == 8 || n == 16) && x && out, FWAV_ERR_ARG, "fwav_debug_dct2: n must be 4, 8 or 16");
+  double tab[2 * (2 * 16 + 11)];
+  dct_constants(n, dbl != 0, tab);
+  auto run = [&](auto tag, auto nn) {
+    using T = decltype(tag);
+    constexpr int N = decltype(nn)::value;
+    DctK<T, N> k;
+    dct_load(k, tab);
+    T c[N];
+    for (int i = 0; i < N; ++i) c[i] = (T)x[i];
+    dct2_ortho<T, N>(c, k);
+    for (int i = 0; i < N; ++i) out[i] = (double)c[i];
+  };
+  using I4 = std::integral_constant<int, 4>;
+  using I8 = std::integral_constant<int, 8>;
+  using I16 = std::integral_constant<int, 16>;
+  if (dbl) {
+    if (n == 4) run(0.0, I4{}); else if (n == 8) run(0.0, I8{}); else run(0.0, I16{});
+  } else {
+    if (n == 4) run(0.0f, I4{}); else if (n == 8) run(0.0f, I8{}); else run(0.0f, I16{});
+  }
   return FWAV_OK;
 }
 

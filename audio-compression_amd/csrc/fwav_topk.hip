@@ -86,10 +86,41 @@ __device__ __forceinline__ void wave_sort_desc(uint64_t (&v)[E]) {
   }
 }
 
-// Sort query ql's buffer, keep the top K, update count and θ.  Whole wave, uniform ql.
+// Exactly equal scores among the first K + 1 entries of a sorted key list (entry e = j·64 + lane, n valid entries):
+// bit 0 — two equal scores inside the top K (numpy's argpartition/argsort decide their order), bit 1 — the K-th and
+// (K+1)-th scores are equal (numpy decides the set).  Scores compare as floats (−0 == +0).  Whole wave; the result
+// is wave-uniform.
+template <int E>
+__device__ __forceinline__ int tie_flags(const uint64_t (&v)[E], int n, int K) {
+  const int lane = threadIdx.x & 63;
+  bool in = false, bd = false;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    uint64_t nx = __shfl_down(v[j], 1);
+    const uint64_t first_next = __shfl(v[j + 1 < E ? j + 1 : j], 0);
+    if (lane == 63) nx = j + 1 < E ? first_next : 0ull;
+    const int e = j * 64 + lane;
+    if (e + 1 < n && e + 1 <= K && key_score(nx) == key_score(v[j])) {
+      if (e + 1 < K) in = true;
+      else bd = true;
+    }
+  }
+  return (__ballot(in) != 0ull ? 1 : 0) | (__ballot(bd) != 0ull ? 2 : 0);
+}
+
+// Lists query qid for the tie check (fwav_tie_check): ties[0] = count, ties[1 + i] = 2·qid + (boundary tie).
+__device__ __forceinline__ void record_tie(int32_t* ties, int32_t qid, int flags) {
+  if (ties != nullptr && flags != 0 && (threadIdx.x & 63) == 0) {
+    const int pos = atomicAdd(ties, 1);
+    ties[1 + pos] = 2 * qid + ((flags >> 1) & 1);
+  }
+}
+
+// Sort query ql's buffer, keep the top K, update count and θ; returns tie_flags of the sorted buffer (a (K+1)-th
+// entry equal to the K-th, about to be dropped, sets bit 1).  Whole wave, uniform ql.
 template <int C>
-__device__ __forceinline__ void compact(uint64_t* __restrict__ keys, int* __restrict__ cnt, float* __restrict__ theta,
-                                        int ql, int K) {
+__device__ __forceinline__ int compact(uint64_t* __restrict__ keys, int* __restrict__ cnt, float* __restrict__ theta,
+                                       int ql, int K) {
   constexpr int E = C / 64;
   const int lane = threadIdx.x & 63;
   const int n = cnt[ql];
@@ -100,6 +131,7 @@ __device__ __forceinline__ void compact(uint64_t* __restrict__ keys, int* __rest
     v[j] = e < n ? keys[ql * C + e] : 0ull;
   }
   wave_sort_desc<E>(v);
+  const int tf = tie_flags<E>(v, n, K);
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
@@ -115,18 +147,21 @@ __device__ __forceinline__ void compact(uint64_t* __restrict__ keys, int* __rest
     cnt[ql] = n < K ? n : K;
     theta[ql] = n >= K ? key_score(kth) : -INFINITY;
   }
+  return tf;
 }
 
 template <int C>
 __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __restrict__ emb, int64_t nd,
                                                                const int32_t* __restrict__ active,
                                                                const int32_t* __restrict__ n_active_p,
-                                                               int64_t q_offset, int K, int32_t* __restrict__ cand) {
+                                                               int64_t q_offset, int K, int32_t* __restrict__ cand,
+                                                               SgemvSplit sp, int32_t* __restrict__ ties) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t* keys = (uint64_t*)smem;                            // [kTopkQ][C]
   float* lda = (float*)(keys + (size_t)kTopkQ * C);            // [kChunk][16] (row-major domain rows)
   int* cnt = (int*)(lda + 16 * kChunk);                        // [kTopkQ]
   float* theta = (float*)(cnt + kTopkQ);                       // [kTopkQ]
+  int* tieb = (int*)(theta + kTopkQ);                          // [kTopkQ] a domain equal to θ was not kept
 
   const int n_active = *n_active_p;
   const int qbase = blockIdx.x * kTopkQ;
@@ -148,6 +183,7 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
   if (tid < kTopkQ) {
     cnt[tid] = 0;
     theta[tid] = -INFINITY;
+    tieb[tid] = 0;
   }
 
   const int64_t nchunks = cdiv(nd, kChunk);
@@ -175,6 +211,10 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
     const int64_t dbase = c * kChunk;
 
     for (int t = 0; t < kChunk / 32; ++t) {
+      // the tile's sgemv kernels (fwav_common.h): all kind 0 unless it holds the tail of a BLAS thread chunk
+      const uint32_t tf0 = (uint32_t)(dbase + t * 32);
+      const uint32_t tl = (uint32_t)min<int64_t>(dbase + t * 32 + 31, nd - 1);
+      const bool plain = sgemv_kind(tl, sp) == 0 && tf0 >= sgemv_chunk_start(tl, sp);
       // the lane's 16 rows of the tile (the row ↔ domain map of the MFMA tiles: d0 + (r&3) + 8*(r>>2))
       floatx16 acc;
 #pragma unroll
@@ -186,7 +226,9 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
           const float4 v = row[j];
           dv[4 * j] = v.x; dv[4 * j + 1] = v.y; dv[4 * j + 2] = v.z; dv[4 * j + 3] = v.w;
         }
-        acc[r] = sgemv16([&](int k) { return dv[k]; }, [&](int k) { return qf[k]; });
+        const uint32_t dr = (uint32_t)(dbase + t * 32 + 4 * h + (r & 3) + 8 * (r >> 2));
+        acc[r] = sgemv16([&](int k) { return dv[k]; }, [&](int k) { return qf[k]; },
+                         plain || dr >= (uint32_t)nd ? 0 : sgemv_kind(dr, sp));
       }
       const int64_t d0 = dbase + t * 32 + 4 * h;  // domain of acc[r] = d0 + (r&3) + 8*(r>>2)
       // mask rows past nd
@@ -198,13 +240,15 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
       float mx = acc[0];
 #pragma unroll
       for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
-      if (__ballot(mx > th) != 0ull) {
+      if (__ballot(mx >= th) != 0ull) {
         uint64_t* kq = keys + (size_t)ql * C;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           if (acc[r] > th) {
             const int slot = atomicAdd(&cnt[ql], 1);
             kq[slot] = make_key(acc[r], (int32_t)(d0 + (r & 3) + 8 * (r >> 2)));
+          } else if (acc[r] == th && th != -INFINITY) {
+            tieb[ql] = 2;  // equal to the K-th but later in index order: not kept, so the set may be numpy's choice
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -212,7 +256,7 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
         while (need != 0ull) {
           const int l = __builtin_ctzll(need);
           need &= need - 1;
-          compact<C>(keys, cnt, theta, wave * 32 + l, K);
+          if (compact<C>(keys, cnt, theta, wave * 32 + l, K) & 2) tieb[wave * 32 + l] = 2;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (q >= 0) th = theta[ql];
@@ -226,7 +270,8 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
     const int qq = qbase + qs;
     if (qq >= n_active) break;
     const int32_t qid = active[qq];
-    compact<C>(keys, cnt, theta, qs, K);
+    const int tf = compact<C>(keys, cnt, theta, qs, K);
+    record_tie(ties, qid, tf | tieb[qs]);
     const int n = cnt[qs];
     int32_t* out = cand + (int64_t)qid * K;
     for (int e = lane; e < K; e += 64) out[e] = e < n ? key_idx(keys[(size_t)qs * C + e]) : -1;
@@ -485,6 +530,7 @@ struct Topk16SmemT {
   int cnt[32 * NG];   // final pass: entries at the front of the query's buffer (its h = 0 lane's appends)
   int cnt1[32 * NG];  // ... and at the back (its h = 1 lane's)
   int ovf[32 * NG];  // band overflowed the buffer (f2key of its band limit, else 0): recompute in exact mode
+  int tie[32 * NG];  // exact mode: a domain scoring exactly the K-th score was not kept (tie_flags bit 1)
   int64_t qrow[32 * NG];
   int32_t qpos[32 * NG];  // position of the slot's query in the active list (index of its shared band limit)
   uint32_t fired[NG][kFifo];                       // deferred work: ring of fired chunk entries
@@ -570,7 +616,8 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0,
 // once (vmcnt(0)), then all key loads and all row loads are issued together (two memory round trips in total).
 template <int C, class SM>
 __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
-                                          const float* __restrict__ emb, int32_t* __restrict__ out) {
+                                          const float* __restrict__ emb, int32_t* __restrict__ out,
+                                          const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid) {
   constexpr int E = C / 64;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -608,12 +655,16 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
       const int j = j0 + jj;
       const int e = j * 64 + lane;
       if (j < E && e < n) {
-        const float acc = sgemv16([&](int k) { return f4c(row[jj][k >> 2], k & 3); }, [&](int k) { return qv[k]; });
+        const float acc = sgemv16([&](int k) { return f4c(row[jj][k >> 2], k & 3); }, [&](int k) { return qv[k]; },
+                                  sgemv_kind((uint32_t)dd[jj], sp));
         v[j] = make_key(acc, dd[jj]);
       }
     }
   }
   wave_sort_desc<E>(v);
+  // exactly tied scores at the top: listed for fwav_tie_check (not for a query about to be searched again)
+  const int tf = tie_flags<E>(v, n, K) | sm.tie[ql];
+  if (sm.ovf[ql] == 0) record_tie(ties, qid, tf);
   // Emit straight from registers (never read back what was just stored: a load issued right behind the stores
   // of the same addresses can return the old contents): the K candidate indices, −1-padded.
 #pragma unroll
@@ -703,7 +754,7 @@ __device__ __forceinline__ int fold16(int r, const floatx16& a) {
 // s16 > S32_K − δ: that is the returned filter limit.
 template <int C>
 __device__ __forceinline__ void compact_exact(uint64_t* __restrict__ kq, int n0, int n1, int K, int& m_out,
-                                              float& lim_out, uint64_t& kth_out) {
+                                              float& lim_out, uint64_t& kth_out, int* __restrict__ tie_slot) {
   constexpr int E = C / 64;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -725,6 +776,17 @@ __device__ __forceinline__ void compact_exact(uint64_t* __restrict__ kq, int n0,
     const int e = j * 64 + lane;
     if (e < K && e < n) kq[e] = v[j];
   }
+  // a dropped (K+1)-th entry with the K-th's score: the set among the equal scores is numpy's choice
+  const int kl1 = K & 63, kj1 = K >> 6;
+  uint32_t kh = 0u, k1h = 0u;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int hj = (int)(uint32_t)(v[j] >> 32);
+    const int a = __shfl(hj, kl), b = __shfl(hj, kl1);
+    if (j == kj) kh = (uint32_t)a;
+    if (j == kj1) k1h = (uint32_t)b;
+  }
+  if (lane == 0 && n > K && key2f(k1h) == key2f(kh)) *tie_slot = 2;
   m_out = n < K ? n : K;
   lim_out = n >= K ? key_score(kth) - kF16Delta : -INFINITY;
   kth_out = n >= K ? kth : 0ull;
@@ -733,7 +795,8 @@ __device__ __forceinline__ void compact_exact(uint64_t* __restrict__ kq, int n0,
 template <int C, bool STATS, class SM, int MODE>
 __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int& qcnt, int& kept, int64_t dt, int64_t nd,
                                              uint64_t* __restrict__ gkeys, SM& sm, int qg, int K, int upd,
-                                             unsigned long long* stats, const float* __restrict__ emb = nullptr,
+                                             unsigned long long* stats, const SgemvSplit& sp,
+                                             const float* __restrict__ emb = nullptr,
                                              const float* qv = nullptr, uint64_t* kthp = nullptr,
                                              uint32_t* __restrict__ share = nullptr) {
   constexpr bool EX = MODE == kModeEX;
@@ -788,7 +851,9 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
         if (on[u]) {
           const int r = rr[u];
           FWAV_TRACE(sm.qrow[ql], 1u, (uint32_t)dt, (uint32_t)((h << 16) | r), (uint32_t)slot);
-          const float sc = sgemv16([&](int k) { return f4c(row[u][k >> 2], k & 3); }, [&](int k) { return qv[k]; });
+          const int64_t dr = dt + 4 * h + (r & 3) + 8 * (r >> 2);
+          const float sc = sgemv16([&](int k) { return f4c(row[u][k >> 2], k & 3); }, [&](int k) { return qv[k]; },
+                                   sgemv_kind((uint32_t)dr, sp));
           const uint32_t uu = __float_as_uint(sc);
           const uint32_t key = uu ^ ((uint32_t)((int32_t)uu >> 31) | 0x80000000u);
           const uint64_t k64 = ((uint64_t)key << 32) | (uint64_t)(nd0 - (uint32_t)((r & 3) + 8 * (r >> 2)));
@@ -797,6 +862,8 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
           if (k64 > *kthp) {
             *reinterpret_cast<uint64_t*>(kbase + (uint32_t)((ql * C + slot) * 8)) = k64;
             slot += step;
+          } else if (key_score(k64) == key_score(*kthp)) {
+            sm.tie[ql] = 2;  // equal to the K-th exact score, later in index order: numpy decides whether it is in
           }
         }
       }
@@ -835,7 +902,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
     uint64_t kth_l = 0;
     if constexpr (EX)
       compact_exact<C>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l),
-                       __builtin_amdgcn_readlane(qcnt, l + 32), K, m, lim, kth_l);
+                       __builtin_amdgcn_readlane(qcnt, l + 32), K, m, lim, kth_l, &sm.tie[qg * 32 + l]);
     else
       compact16_s16<C, MODE == kModeHL>(gkeys + (size_t)(qg * 32 + l) * C, __builtin_amdgcn_readlane(qcnt, l),
                        __builtin_amdgcn_readlane(qcnt, l + 32), sm, qg * 32 + l, K, STATS ? stats : nullptr, m, lim);
@@ -897,8 +964,9 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
                                                half8 b, half8 bl, float thf, int& qcnt,
                                                int& kept, ReplayCursor& cur, int tail, int64_t nd, uint64_t* __restrict__ gkeys,
                                                SM& sm, int qg, int K, int upd, unsigned long long* stats,
-                                               const float* __restrict__ emb = nullptr, const float* qv = nullptr,
-                                               uint64_t* kthp = nullptr, uint32_t* __restrict__ share = nullptr) {
+                                               const SgemvSplit& sp, const float* __restrict__ emb = nullptr,
+                                               const float* qv = nullptr, uint64_t* kthp = nullptr,
+                                               uint32_t* __restrict__ share = nullptr) {
   constexpr bool HL = MODE == kModeHL;
   const int lane = threadIdx.x & 63;
   const int col = lane & 31;
@@ -935,8 +1003,8 @@ __device__ __forceinline__ float replay_window(const _Float16* __restrict__ emb1
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], bl, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl[u], b, acc, 0, 0, 0);
       }
-      thf = append_tile<C, STATS, SM, MODE>(acc, thf, qcnt, kept, ct[u], nd, gkeys, sm, qg, K, upd, stats, emb, qv,
-                                          kthp, share);
+      thf = append_tile<C, STATS, SM, MODE>(acc, thf, qcnt, kept, ct[u], nd, gkeys, sm, qg, K, upd, stats, sp, emb,
+                                          qv, kthp, share);
     }
     if (ct[kReplayBatch - 1] < 0) break;
   }
@@ -1087,7 +1155,8 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
                                                                 uint32_t* __restrict__ share_lim,
                                                                 const uint32_t* __restrict__ seeds_in,
                                                                 float seed_shift, int plan_rt,
-                                                                int plan_p, int dbg, unsigned long long* gstats) {
+                                                                int plan_p, int dbg, unsigned long long* gstats,
+                                                                SgemvSplit sp, int32_t* __restrict__ ties) {
   constexpr bool EX = MODE == kModeEX;
   constexpr bool HL = MODE == kModeHL;
   constexpr int NG = W * QS;  // query groups of 32 per workgroup; wave w owns groups w·QS .. w·QS + QS − 1
@@ -1157,6 +1226,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
     qpos[s] = (int32_t)(qi < n_active ? qi : 0);
     if (h == 0) {
       sm.ovf[ql] = 0;
+      sm.tie[ql] = 0;
       sm.qrow[ql] = qrow;
       sm.qpos[ql] = qpos[s];
     }
@@ -1291,7 +1361,8 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
       for (int s = 0; s < QS; ++s) {
         if (nfired[s] > cur[s].head || cur[s].rem != 0u)
           thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s], qcnt[s], kept[s], cur[s],
-                                           nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, emb, qv[s], &kth[s], share);
+                                           nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, sp, emb, qv[s], &kth[s],
+                                           share);
       }
       if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
       // retire the replay's loads and stores here, visibly to hipcc's wait bookkeeping (vmcnt(0) expcnt(7)
@@ -1322,7 +1393,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
       continue;
     }
     // exact f32 rescoring of the kept band + sort
-    compact16<C>(kq, sm, qs, K, emb, cand + (int64_t)qid * K);
+    compact16<C>(kq, sm, qs, K, emb, cand + (int64_t)qid * K, sp, ties, qid);
     // overflowed: listed for the exact-mode relaunch with its band limit as the seed (same list position)
     if (lane == 0 && sm.ovf[qs]) {
       const int pos = atomicAdd(n_ovf, 1);
@@ -1356,7 +1427,8 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
                                                       const int32_t* __restrict__ n_active_p, int plan_rt, int plan_p,
                                                       int K, int32_t* __restrict__ cand, int32_t* __restrict__ ovf_list,
                                                       int32_t* __restrict__ n_ovf, const uint32_t* __restrict__ share,
-                                                      const float* __restrict__ emb, int64_t q_offset) {
+                                                      const float* __restrict__ emb, int64_t q_offset, SgemvSplit sp,
+                                                      int32_t* __restrict__ ties) {
   constexpr int E = C / 64;
   const int n_active = *n_active_p;
   const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
@@ -1460,11 +1532,13 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
       float4 row[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) row[i] = rp[i];
-      const float acc = sgemv16([&](int k) { return f4c(row[k >> 2], k & 3); }, [&](int k) { return qv[k]; });
+      const float acc = sgemv16([&](int k) { return f4c(row[k >> 2], k & 3); }, [&](int k) { return qv[k]; },
+                                sgemv_kind((uint32_t)d, sp));
       v[j] = make_key(acc, d);
     }
   }
   wave_sort_desc<E>(v);
+  record_tie(ties, qid, tie_flags<E>(v, mb < C ? mb : C, K));
   int32_t* out = cand + (int64_t)qid * K;
 #pragma unroll
   for (int j = 0; j < E; ++j) {
@@ -1575,14 +1649,16 @@ static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
 
 template <int C>
 static size_t topk_lds_bytes() {
-  return (size_t)kTopkQ * C * sizeof(uint64_t) + 16 * kChunk * sizeof(float) + 2 * kTopkQ * sizeof(int);
+  return (size_t)kTopkQ * C * sizeof(uint64_t) + 16 * kChunk * sizeof(float) + 3 * kTopkQ * sizeof(int);
 }
 
 template <int C>
 static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, const int32_t* active,
                        const int32_t* n_active, int64_t max_q, int64_t q_offset, int K, int32_t* cand, hipStream_t st,
-                       uint64_t* gkeys, int dbg = 0, unsigned long long* stats = nullptr) {
+                       uint64_t* gkeys, SgemvSplit sp, int32_t* ties, int dbg = 0,
+                       unsigned long long* stats = nullptr) {
   const int64_t grid = cdiv(max_q, kTopkQ);
+  if (ties != nullptr) (void)hipMemsetAsync(ties, 0, sizeof(int32_t), st);
   if (grid == 0) return FWAV_OK;
   if (emb16 != nullptr) {
     if (gkeys == nullptr) {
@@ -1614,10 +1690,12 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     const int mode1 = first_mode(nd);
 #define FWAV_FIRST(MODE_, STATS_, DBG_, ST_)                                                                    \
   k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, 0, st>>>(                                 \
-      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, DBG_, ST_)
+      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, DBG_, ST_,  \
+      sp, ties)
 #define FWAV_FIRST_WIDE(MODE_)                                                                                   \
   k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG><<<pl.items(), 64 * kWideW, 0, st>>>(                    \
-      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr)
+      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
+      sp, ties)
 #ifdef FWAV_TOPK_EXTSEED
     if (stats != nullptr && dbg == 0) {
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
@@ -1636,7 +1714,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     if (pl.R > 0) {
 #define FWAV_MERGE(QB_, HL_)                                                                                    \
   k_merge_pieces<k16Cap, QB_, HL_><<<cdiv(pl.R * QB_, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, \
-                                                                       ovf1, n_ovf1, share, emb, q_offset)
+                                                                       ovf1, n_ovf1, share, emb, q_offset, sp, ties)
       if (wide) {
         if (mode1 == kModeHL) FWAV_MERGE(kWideQB, true); else FWAV_MERGE(kWideQB, false);
       } else {
@@ -1655,7 +1733,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     if (mode1 == kModeS16) {
       k_sim_topk_f16<k16Cap, false, kModeHL><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, ovf1, n_ovf1, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, seeds1, kStreamMargin, 0, 1, 0,
-          nullptr);
+          nullptr, sp, ties);
       ex_in = ovf2;
       ex_n = n_ovf2;
       ex_seeds = seeds2;
@@ -1663,11 +1741,11 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     if (stats != nullptr && (dbg & (1 << 17)))  // diagnostic: counters of the exact-mode relaunch only
       k_sim_topk_f16<k16Cap, true, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, ex_seeds, kStreamMargin, 0, 1, 0,
-          stats);
+          stats, sp, ties);
     else
       k_sim_topk_f16<k16Cap, false, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, ex_seeds, kStreamMargin, 0, 1, 0,
-          nullptr);
+          nullptr, sp, ties);
   } else {
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32[kMaxDev] = {false};  // a function attribute is set per device
@@ -1676,7 +1754,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       (void)hipFuncSetAttribute((const void*)k_sim_topk_f32<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr32[dev] = true;
     }
-    k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, active, n_active, q_offset, K, cand);
+    k_sim_topk_f32<C><<<grid, kTopkThreads, lds, st>>>(emb, nd, active, n_active, q_offset, K, cand, sp, ties);
   }
   FWAV_LAUNCH_CHECK("fwav_sim_topk");
   return FWAV_OK;
@@ -1686,7 +1764,9 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
 int64_t large_batch(int64_t nd, int64_t max_q);
 size_t large_workspace_bytes(int64_t nd, int64_t max_q);
 int launch_topk_large(const float* emb, int64_t nd, const int32_t* active, const int32_t* n_active, int64_t max_q,
-                      int64_t q_offset, int K, int32_t* cand, float* S, hipStream_t st);
+                      int64_t q_offset, int K, int32_t* cand, float* S, SgemvSplit sp, int32_t* ties, hipStream_t st);
+int launch_score_rows(const float* emb, int64_t nd, const int32_t* rows, int64_t n_rows, int64_t q_offset,
+                      SgemvSplit sp, float* S, hipStream_t st);
 
 }  // namespace fwav
 
@@ -1709,9 +1789,10 @@ size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
 // not listed are not touched.  emb16 (tiled fp16 copy from fwav_pool_embed) selects the fp16 pre-filter
 // kernel; NULL runs the all-f32-MFMA kernel.  Both return identical candidates.
 int fwav_sim_topk(const float* emb, const void* emb16, int64_t nd, const int32_t* active, const int32_t* n_active,
-                  int64_t max_q, int64_t q_offset, int K, int32_t* cand, void* workspace, size_t ws_bytes,
-                  void* stream) {
+                  int64_t max_q, int64_t q_offset, int K, int blas_threads, int32_t* cand, int32_t* ties,
+                  void* workspace, size_t ws_bytes, void* stream) {
   FWAV_CHECK_ARG(emb && active && n_active && cand && nd > 0 && max_q >= 0, FWAV_ERR_ARG, "fwav_sim_topk: bad args");
+  FWAV_CHECK_ARG(blas_threads >= 1 && blas_threads <= 4096, FWAV_ERR_ARG, "fwav_sim_topk: blas_threads outside [1, 4096]");
   FWAV_CHECK_ARG(K >= 1 && K <= fwav_topk_max_k(), FWAV_ERR_K, "fwav_sim_topk: K=%d outside [1, %d]", K,
                  fwav_topk_max_k());
   FWAV_CHECK_ARG(nd < (int64_t)0x7fffffff, FWAV_ERR_SHAPE, "fwav_sim_topk: nd too large");
@@ -1719,13 +1800,27 @@ int fwav_sim_topk(const float* emb, const void* emb16, int64_t nd, const int32_t
   if (K > 64) {
     FWAV_CHECK_ARG(workspace && ws_bytes >= fwav_sim_topk_workspace_size(max_q, nd, K), FWAV_ERR_WORKSPACE,
                    "fwav_sim_topk: workspace too small");
+    if (ties != nullptr) (void)hipMemsetAsync(ties, 0, sizeof(int32_t), st);
     if (max_q == 0) return FWAV_OK;
-    return launch_topk_large(emb, nd, active, n_active, max_q, q_offset, K, cand, (float*)workspace, st);
+    return launch_topk_large(emb, nd, active, n_active, max_q, q_offset, K, cand, (float*)workspace,
+                             make_sgemv_split(nd, blas_threads), ties, st);
   }
   FWAV_CHECK_ARG(emb16 == nullptr || (workspace && ws_bytes >= fwav_sim_topk_workspace_size(max_q, nd, K)),
                  FWAV_ERR_WORKSPACE, "fwav_sim_topk: workspace too small");
   return launch_topk<128>(emb, (const _Float16*)emb16, nd, active, n_active, max_q, q_offset, K, cand, st,
-                          (uint64_t*)workspace);
+                          (uint64_t*)workspace, make_sgemv_split(nd, blas_threads), ties);
+}
+
+// Exact reference score rows for the host's tie resolution: scores[i·nd + d] = emb[d] · emb[q_offset + rows[i]] in
+// the reference's sgemv order for `blas_threads` OpenBLAS threads (fractal.py:537).
+int fwav_score_rows(const float* emb, int64_t nd, const int32_t* rows, int64_t n_rows, int64_t q_offset,
+                    int blas_threads, float* scores, void* stream) {
+  FWAV_CHECK_ARG(emb && rows && scores && nd > 0 && nd < (int64_t)0x7fffffff && n_rows >= 0, FWAV_ERR_ARG,
+                 "fwav_score_rows: bad args");
+  FWAV_CHECK_ARG(blas_threads >= 1 && blas_threads <= 4096, FWAV_ERR_ARG, "fwav_score_rows: blas_threads outside [1, 4096]");
+  if (n_rows == 0) return FWAV_OK;
+  return launch_score_rows(emb, nd, rows, n_rows, q_offset, make_sgemv_split(nd, blas_threads), scores,
+                           (hipStream_t)stream);
 }
 
 // Diagnostic ablations of the fp16 search kernel (timing only; see k_sim_topk_f16 `dbg`).
@@ -1734,7 +1829,7 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t nd, const i
                         unsigned long long* stats, void* stream) {
   FWAV_CHECK_ARG(emb && emb16 && workspace && K >= 1 && K <= 64, FWAV_ERR_ARG, "fwav_debug_sim_topk: bad args");
   return launch_topk<128>(emb, (const _Float16*)emb16, nd, active, n_active, max_q, q_offset, K, cand,
-                          (hipStream_t)stream, (uint64_t*)workspace, dbg, stats);
+                          (hipStream_t)stream, (uint64_t*)workspace, make_sgemv_split(nd, 1), nullptr, dbg, stats);
 }
 
 #ifdef FWAV_TOPK_DEBUG

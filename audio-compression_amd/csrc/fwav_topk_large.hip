@@ -29,15 +29,15 @@ constexpr int kScoreThreads = 256;
 constexpr int kScoreQ = 32;            // queries per k_scores_batch pass (q vectors in LDS)
 constexpr size_t kLargeBudget = size_t(1) << 30;  // score-row workspace budget (bytes)
 
-__device__ __forceinline__ float score_chain(const float (&e)[16], const float* __restrict__ q) {
-  return sgemv16([&](int k) { return e[k]; }, [&](int k) { return q[k]; });
+__device__ __forceinline__ float score_chain(const float (&e)[16], const float* __restrict__ q, int kind) {
+  return sgemv16([&](int k) { return e[k]; }, [&](int k) { return q[k]; }, kind);
 }
 
 // S[j·nd + d] = score(domain d, query active[qb + j]) for j < B (rows of queries past n_active untouched).
 __global__ __launch_bounds__(kScoreThreads) void k_scores_batch(const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
                                                                 const int32_t* __restrict__ n_active_p,
-                                                                int64_t qb, int B, int64_t q_offset,
+                                                                int64_t qb, int B, int64_t q_offset, SgemvSplit sp,
                                                                 float* __restrict__ S) {
   __shared__ float qv[kScoreQ][16];
   const int n_active = *n_active_p;
@@ -61,8 +61,39 @@ __global__ __launch_bounds__(kScoreThreads) void k_scores_batch(const float* __r
       qv[t / 16][t % 16] = emb[q * 16 + t % 16];
     }
     __syncthreads();
+    if (d < nd) {
+      const int kind = sgemv_kind((uint32_t)d, sp);
+      for (int j = 0; j < m; ++j) S[(int64_t)(j0 + j) * nd + d] = score_chain(e, qv[j], kind);
+    }
+  }
+}
+
+// S[i·nd + d] = score(domain d, query row q_offset + rows[i]), i < n_rows (fwav_score_rows).
+__global__ __launch_bounds__(kScoreThreads) void k_score_rows(const float* __restrict__ emb, int64_t nd,
+                                                              const int32_t* __restrict__ rows, int n_rows,
+                                                              int64_t q_offset, SgemvSplit sp, float* __restrict__ S) {
+  __shared__ float qv[kScoreQ][16];
+  const int64_t d = (int64_t)blockIdx.x * kScoreThreads + threadIdx.x;
+  float e[16];
+  if (d < nd) {
+    const float4* p = reinterpret_cast<const float4*>(emb + d * 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 v = p[j];
+      e[4 * j] = v.x; e[4 * j + 1] = v.y; e[4 * j + 2] = v.z; e[4 * j + 3] = v.w;
+    }
+  }
+  const int kind = d < nd ? sgemv_kind((uint32_t)d, sp) : 0;
+  for (int j0 = 0; j0 < n_rows; j0 += kScoreQ) {
+    const int m = min(kScoreQ, n_rows - j0);
+    __syncthreads();
+    for (int t = threadIdx.x; t < m * 16; t += kScoreThreads) {
+      const int64_t q = (int64_t)rows[j0 + t / 16] + q_offset;
+      qv[t / 16][t % 16] = emb[q * 16 + t % 16];
+    }
+    __syncthreads();
     if (d < nd)
-      for (int j = 0; j < m; ++j) S[(int64_t)(j0 + j) * nd + d] = score_chain(e, qv[j]);
+      for (int j = 0; j < m; ++j) S[(int64_t)(j0 + j) * nd + d] = score_chain(e, qv[j], kind);
   }
 }
 
@@ -94,6 +125,7 @@ struct SelSmem {
   uint64_t list[kCap];
   uint32_t hist[256];
   int cnt;
+  int tflag;  // tie_flags of the query (fwav_topk.hip): 1 = equal scores inside the top K, 2 = at the K-th place
   int wtot[kSelThreads / 64];
   uint32_t bcast[4];
 };
@@ -146,6 +178,8 @@ __device__ void radix_select_collect(const float* __restrict__ row, int64_t nd, 
     prefix |= sm.bcast[0] << shift;
     pmask |= 255u << shift;
     krem -= (int)sm.bcast[1];
+    // last pass: hist[b] keys equal T exactly; more of them than the top K takes → the set is numpy's choice
+    if (pass == 3 && threadIdx.x == 0 && (int)sm.hist[sm.bcast[0]] > krem) sm.tflag |= 2;
     __syncthreads();
   }
   const uint32_t T = prefix;
@@ -193,11 +227,13 @@ __device__ void radix_select_collect(const float* __restrict__ row, int64_t nd, 
 __global__ __launch_bounds__(kSelThreads) void k_select(const float* __restrict__ S, int64_t nd,
                                                         const int32_t* __restrict__ active,
                                                         const int32_t* __restrict__ n_active_p, int64_t qb, int K,
-                                                        int32_t* __restrict__ cand) {
+                                                        int32_t* __restrict__ cand, int32_t* __restrict__ ties) {
   __shared__ SelSmem sm;
   const int n_active = *n_active_p;
   const int64_t qi = qb + blockIdx.x;
   if (qi >= n_active) return;
+  if (threadIdx.x == 0) sm.tflag = 0;
+  __syncthreads();
   const float* row = S + (int64_t)blockIdx.x * nd;
   int32_t* out = cand + (int64_t)active[qi] * K;
   int n;  // valid entries in sm.list
@@ -250,6 +286,15 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const float* __restrict_
   while (p2 < n) p2 <<= 1;
   for (int i = n + threadIdx.x; i < p2; i += kSelThreads) sm.list[i] = 0ull;
   block_sort_desc(sm.list, p2);
+  // exactly equal scores among the first K + 1 (for nd ≤ K: among all), listed for fwav_tie_check
+  for (int e = threadIdx.x; e + 1 < n && e + 1 <= K; e += kSelThreads)
+    if (key2f((uint32_t)(sm.list[e] >> 32)) == key2f((uint32_t)(sm.list[e + 1] >> 32)))
+      atomicOr(&sm.tflag, e + 1 < K ? 1 : 2);
+  __syncthreads();
+  if (threadIdx.x == 0 && ties != nullptr && sm.tflag != 0) {
+    const int pos = atomicAdd(ties, 1);
+    ties[1 + pos] = 2 * active[qi] + ((sm.tflag >> 1) & 1);
+  }
   for (int e = threadIdx.x; e < K; e += kSelThreads) out[e] = e < n ? (int32_t)(~(uint32_t)(sm.list[e] & 0xffffffffu)) : -1;
 }
 
@@ -264,14 +309,25 @@ int64_t large_batch(int64_t nd, int64_t max_q) {
 size_t large_workspace_bytes(int64_t nd, int64_t max_q) { return (size_t)large_batch(nd, max_q) * nd * 4; }
 
 int launch_topk_large(const float* emb, int64_t nd, const int32_t* active, const int32_t* n_active, int64_t max_q,
-                      int64_t q_offset, int K, int32_t* cand, float* S, hipStream_t st) {
+                      int64_t q_offset, int K, int32_t* cand, float* S, SgemvSplit sp, int32_t* ties, hipStream_t st) {
   const int64_t B = large_batch(nd, max_q);
   for (int64_t qb = 0; qb < max_q; qb += B) {
     k_scores_batch<<<cdiv(nd, kScoreThreads), kScoreThreads, 0, st>>>(emb, nd, active, n_active, qb, (int)B,
-                                                                       q_offset, S);
-    k_select<<<B, kSelThreads, 0, st>>>(S, nd, active, n_active, qb, K, cand);
+                                                                       q_offset, sp, S);
+    k_select<<<B, kSelThreads, 0, st>>>(S, nd, active, n_active, qb, K, cand, ties);
   }
   FWAV_LAUNCH_CHECK("fwav_sim_topk (large K)");
+  return FWAV_OK;
+}
+
+int launch_score_rows(const float* emb, int64_t nd, const int32_t* rows, int64_t n_rows, int64_t q_offset,
+                      SgemvSplit sp, float* S, hipStream_t st) {
+  for (int64_t r0 = 0; r0 < n_rows; r0 += 4096) {
+    const int m = (int)std::min<int64_t>(4096, n_rows - r0);
+    k_score_rows<<<cdiv(nd, kScoreThreads), kScoreThreads, 0, st>>>(emb, nd, rows + r0, m, q_offset, sp,
+                                                                     S + r0 * nd);
+  }
+  FWAV_LAUNCH_CHECK("fwav_score_rows");
   return FWAV_OK;
 }
 

@@ -8,6 +8,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+from . import _digest
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfwav.so")
 
@@ -22,6 +24,7 @@ SZ = C.c_size_t
 SIGNATURES = {
     "fwav_last_error": (C.c_char_p, []),
     "fwav_abi_version": (I32, []),
+    "fwav_build_digest": (C.c_char_p, []),
     "fwav_stream_sync": (I32, [P]),
     "fwav_voiced_workspace_size": (SZ, [I64, I32]),
     "fwav_voiced_ranges": (I32, [P, I64, I32, I32, I32, F32, F32, P, I64, P, P, SZ, P]),
@@ -30,12 +33,15 @@ SIGNATURES = {
     "fwav_weighted_energy": (I32, [P, I64, P, P, SZ, P]),
     "fwav_prune": (I32, [P, I64, I64, I32, F32, I32, P, I64, I32, P, P, P, P, P]),
     "fwav_emb16_elems": (SZ, [I64]),
+    "fwav_embed_tables_size": (SZ, [I32]),
     "fwav_embed_tables": (I32, [I32, P]),
+    "fwav_debug_dct2": (I32, [I32, I32, P, P]),
     "fwav_pool_workspace_size": (SZ, [I64, I32, I32, I32]),
     "fwav_pool_embed": (I32, [P, I64, I32, I32, I32, P, P, P, P, P, SZ, P]),
     "fwav_topk_max_k": (I32, []),
     "fwav_sim_topk_workspace_size": (SZ, [I64, I64, I32]),
-    "fwav_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, SZ, P]),
+    "fwav_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, I32, P, P, P, SZ, P]),
+    "fwav_score_rows": (I32, [P, I64, P, I64, I64, I32, P, P]),
     "fwav_debug_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, I32, P, P]),
     "fwav_debug_topk_plan": (I32, [I32, I32]),
     "fwav_debug_topk_plan_cover": (I32, [I64, I32, I32, I32, P, P]),
@@ -43,6 +49,7 @@ SIGNATURES = {
     "fwav_debug_topk_geometry": (I32, [I32]),
     "fwav_debug_gather_rows": (I32, [P, I64, I32, I64, P, P]),
     "fwav_affine": (I32, [P, I64, I32, P, I32, P, I64, F32, P, P, P, P, P, P]),
+    "fwav_tie_check": (I32, [P, I64, I32, P, I32, P, I64, P, I64, I32, P, I64, P, P]),
     "fwav_decode_workspace_size": (SZ, [I64, I32, I32]),
     "fwav_decode": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, SZ, P]),
     "fwav_decode_span": (I32, []),
@@ -68,6 +75,12 @@ def lib() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise FwavError(f"HIP library not built: {LIB_PATH} is missing (run __graft_entry__.build())")
         dll = C.CDLL(LIB_PATH)
+        dll.fwav_build_digest.restype = C.c_char_p
+        built = dll.fwav_build_digest().decode()
+        want = _digest.source_digest()
+        if want is not None and built != want:
+            raise FwavError(f"{LIB_PATH} was built from other sources (digest {built[:12]}, sources {want[:12]}): "
+                            "run __graft_entry__.build()")
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(dll, name)
             fn.restype = res

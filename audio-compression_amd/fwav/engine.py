@@ -9,7 +9,7 @@ Reference map (``/root/reference/fractal.py``):
   silent-input test :1083                                  → fwav_weighted_energy (f64 partials)
   build_domains_memmap :285-334 + build_domain_embeddings :238-280 → fwav_pool_embed
   cpu_worker energy prune :601-603, pad :622               → fwav_prune
-  linear top-K :535-541, 617-620                           → fwav_sim_topk
+  linear top-K :535-541, 617-620                           → fwav_sim_topk (+ fwav_tie_check / fwav.ties for exact ties)
   _process_gpu_batch :757-850                              → fwav_affine
   decompress_audio :1378-1473                              → fwav_decode
 """
@@ -22,7 +22,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, ties as _ties
 from ._lib import FwavError, call, size_call
 
 F32 = np.float32
@@ -59,7 +59,7 @@ _TABLES: dict = {}
 def embed_tables(rs: int, device: torch.device) -> torch.Tensor:
     key = (rs, str(device))
     if key not in _TABLES:
-        host = np.zeros(16 * rs, np.float64)
+        host = np.zeros(size_call("fwav_embed_tables_size", rs), np.float64)
         call("fwav_embed_tables", rs, host.ctypes.data)
         _TABLES[key] = torch.from_numpy(host).to(device)
     return _TABLES[key]
@@ -123,6 +123,8 @@ class DeviceCompressed:
     err: Optional[torch.Tensor] = None
     n_active: Optional[torch.Tensor] = None
     energy_partial: Optional[torch.Tensor] = None
+    n_ties: int = 0          # queries whose top K + 1 scores hold exact ties
+    n_resolved: int = 0      # of those, rows re-ranked with numpy's own tie order (fwav.ties)
     empty: bool = False
 
     def is_silent(self) -> bool:
@@ -156,7 +158,8 @@ def compress_device(sig: torch.Tensor, *args, **kwargs) -> DeviceCompressed:
 def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thresh: float = 1e-4,
                      fast_mode: bool = True, s_clip: float = 16.0, shard: Optional[tuple[int, int]] = None,
                      keep_intermediates: bool = False, events: Optional[dict] = None,
-                     search: str = "f16", on_pool=None) -> DeviceCompressed:
+                     search: str = "f16", on_pool=None, blas_threads: Optional[int] = None,
+                     tie_order: str = "numpy") -> DeviceCompressed:
     """Run the compress hot path on ``sig`` (1-D float32 tensor on a HIP device).
 
     ``shard=(lo, hi)`` restricts candidate search and the affine solve to ranges ``[lo, hi)`` (the
@@ -166,6 +169,10 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     whole signal.  Raises ValueError for the reference's own error cases (empty input; n_ranges >
     n_domains).  ``on_pool(pool)``, when given, is called right after the pool kernel is queued (the API
     starts the pool's device→host copy there, on a side stream, so that it overlaps the search).
+    ``blas_threads``: the OpenBLAS thread count whose sgemv order the scores follow (default: this process's,
+    fwav.ties.blas_threads).  ``tie_order="numpy"`` re-ranks the rows whose match depends on the order of exactly
+    equal scores with numpy's own calls, as the reference does (one host synchronisation to read the count);
+    ``"index"`` keeps the device's (score desc, index asc) order for them (no synchronisation).
     """
     if sig.dim() != 1 or sig.dtype != torch.float32 or not sig.is_cuda:
         raise ValueError("compress_device expects a 1-D float32 device tensor")
@@ -185,6 +192,9 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     lo32 = F32(energy_thresh * 0.5)
     if k > size_call("fwav_topk_max_k"):
         raise ValueError(f"top_k={k} > {size_call('fwav_topk_max_k')} is not supported by the HIP search")
+    if tie_order not in ("numpy", "index"):
+        raise ValueError("tie_order must be 'numpy' (the reference's order of exactly tied scores) or 'index'")
+    threads = _ties.blas_threads() if blas_threads is None else int(blas_threads)
     ws_n = size_call("fwav_voiced_workspace_size", n, frame)
     ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
     ranges = torch.empty(nr * rs, dtype=torch.float32, device=dev)
@@ -243,13 +253,28 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
         _mark(events, "sim_topk")
         wk = size_call("fwav_sim_topk_workspace_size", m, nd, k) if (emb16 is not None or k > 64) else 0
         wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
-        call("fwav_sim_topk", emb.data_ptr(), _p(emb16), nd, active.data_ptr(), n_active.data_ptr(), m, lo, k,
-             cand.data_ptr(), wsk.data_ptr(), wk, st)
+        ties = torch.empty(m + 1, dtype=torch.int32, device=dev) if tie_order == "numpy" else None
+        call("fwav_sim_topk", emb.data_ptr(), _p(emb16), nd, active.data_ptr(), n_active.data_ptr(), m, lo, k, threads,
+             cand.data_ptr(), _p(ties), wsk.data_ptr(), wk, st)
         _mark(events, "sim_topk")
         _mark(events, "affine")
-        call("fwav_affine", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd,
-             float(abs(F32(s_clip))), idx.data_ptr(), s.data_ptr(), o.data_ptr(), sym.data_ptr(), err.data_ptr(), st)
+        sc = float(abs(F32(s_clip)))
+        call("fwav_affine", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, sc, idx.data_ptr(),
+             s.data_ptr(), o.data_ptr(), sym.data_ptr(), err.data_ptr(), st)
         _mark(events, "affine")
+        if ties is not None:
+            # exactly tied scores whose order can change a match: numpy's own ranking for those rows (fwav.ties)
+            _mark(events, "ties")
+            resolve = torch.empty(m + 1, dtype=torch.int32, device=dev)
+            call("fwav_tie_check", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, emb.data_ptr(), lo,
+                 threads, ties.data_ptr(), m, resolve.data_ptr(), st)
+            counts = torch.stack([ties[0], resolve[0]]).cpu()
+            res.n_ties, res.n_resolved = int(counts[0]), int(counts[1])
+            if res.n_resolved:
+                _ties.resolve_rows(resolve[1:1 + res.n_resolved], emb=emb, n_domains=nd, q_offset=lo, k=k,
+                                   threads=threads, ranges=rsh, range_size=rs, pool=pool, s_clip=sc, cand=cand,
+                                   outs=(idx, s, o, sym, err), stream=st)
+            _mark(events, "ties")
     res.pool, res.idx, res.s, res.o, res.sym, res.err, res.n_active = pool, idx, s, o, sym, err, n_active
     if keep_intermediates:
         res.ranges, res.emb, res.cand, res.active = ranges, emb, cand, active

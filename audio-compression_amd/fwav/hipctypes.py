@@ -103,7 +103,7 @@ def pool_embed(signal: np.ndarray, tile: int, rs: int, step: int):
     sig = np.ascontiguousarray(signal, np.float32)
     n = sig.size
     nd = (n - tile) // step + 1
-    tab = np.empty(16 * rs, np.float64)
+    tab = np.empty(size_call("fwav_embed_tables_size", rs), np.float64)
     call("fwav_embed_tables", rs, tab.ctypes.data)
     ds, dt = DeviceBuffer.from_array(sig), DeviceBuffer.from_array(tab)
     dpool, demb = DeviceBuffer(4 * nd * rs), DeviceBuffer(4 * nd * 16)

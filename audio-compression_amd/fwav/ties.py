@@ -1,0 +1,101 @@
+"""Exactly tied similarity scores: the reference's numpy tie order, reproduced where it can change a match.
+
+The reference ranks each range's candidates with numpy (fractal.py:535-541)::
+
+    scores = domain_embs @ q
+    idxs = np.argpartition(scores, -top_k)[-top_k:]
+    return idxs[np.argsort(scores[idxs])[::-1]]
+
+so among exactly equal scores its order — and, when the K-th and (K+1)-th scores are equal, its candidate set — is
+whatever numpy's selection and sort (x86-simd-sort on this image's CPUs) leave them in: a function of the whole
+score row, not of the tied values alone.  The device search emits (score desc, index asc) and lists every query
+whose top K + 1 scores hold a tie (``fwav_sim_topk`` ``ties``); ``fwav_tie_check`` keeps those whose match could
+depend on the order (a tie at the K-th place, or two candidates of one run of equal scores that both attain the
+minimum error).  For them — none on noise, a handful of rows on speech, many on periodic signals — this module
+takes the exact score row (``fwav_score_rows``, the reference's own sgemv order), runs the reference's own numpy
+calls on it (:func:`numpy_topk_row`), and re-solves those rows with ``fwav_affine``.  Every value still comes from
+the device; numpy only orders equal keys, exactly as it does in the reference.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ._lib import call
+
+#: host bytes of exact score rows fetched per batch
+ROW_BUDGET = 256 << 20
+
+_BLAS_THREADS = None
+
+
+def blas_threads() -> int:
+    """OpenBLAS's thread count in this process — the split of the reference's sgemv that decides which domains its
+    tail kernels score (fwav_common.h).  The reference would run here with the same numpy, so its scores follow this
+    count; ``FWAV_BLAS_THREADS`` overrides it."""
+    global _BLAS_THREADS
+    env = os.environ.get("FWAV_BLAS_THREADS")
+    if env:
+        return max(1, int(env))
+    if _BLAS_THREADS is None:
+        n = None
+        try:
+            import threadpoolctl
+            for info in threadpoolctl.threadpool_info():
+                if info.get("user_api") == "blas":
+                    n = int(info["num_threads"])
+                    break
+        except Exception:  # noqa: BLE001
+            n = None
+        _BLAS_THREADS = max(1, n if n else (os.cpu_count() or 1))
+    return _BLAS_THREADS
+
+
+def numpy_topk_row(scores: np.ndarray, k: int) -> np.ndarray:
+    """range_candidates_from_embedding_emb (fractal.py:535-541) + pad_candidates (:544-552) on one score row, by the
+    reference's own numpy calls."""
+    nd = len(scores)
+    if k >= nd:
+        idx = np.argsort(scores)[::-1]
+    else:
+        part = np.argpartition(scores, -k)[-k:]
+        idx = part[np.argsort(scores[part])[::-1]]
+    out = np.full(k, -1, np.int32)
+    out[:min(k, len(idx))] = idx[:k]
+    return out
+
+
+def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, k: int, threads: int,
+                 ranges: torch.Tensor, range_size: int, pool: torch.Tensor, s_clip: float, cand: torch.Tensor,
+                 outs: tuple, stream: int) -> None:
+    """Rows (local indices, device int32) whose match depends on numpy's tie order: exact score rows in batches,
+    numpy's ranking on the host, the new candidate rows written back to ``cand`` and the affine solve re-run for those
+    rows into ``outs`` = (idx, s, o, sym, err)."""
+    dev = rows.device
+    n = rows.numel()
+    if n == 0:
+        return
+    nd = int(n_domains)
+    per = max(1, min(n, ROW_BUDGET // (4 * nd)))
+    cv = cand.view(-1, k)
+    new_rows = []
+    for b0 in range(0, n, per):
+        rb = rows[b0:b0 + per].contiguous()
+        m = rb.numel()
+        S = torch.empty(m * nd, dtype=torch.float32, device=dev)
+        call("fwav_score_rows", emb.data_ptr(), nd, rb.data_ptr(), m, int(q_offset), int(threads), S.data_ptr(),
+             stream)
+        Sh = S.view(m, nd).cpu().numpy()
+        new_rows.append(np.stack([numpy_topk_row(Sh[i], k) for i in range(m)]))
+    newc = torch.from_numpy(np.concatenate(new_rows)).to(dev)
+    ridx = rows.long()
+    cv[ridx] = newc
+    rs = int(range_size)
+    rsub = ranges.view(-1, rs)[ridx].contiguous()
+    tmp = [torch.empty(n, dtype=t.dtype, device=dev) for t in outs]
+    call("fwav_affine", rsub.data_ptr(), n, rs, newc.data_ptr(), k, pool.data_ptr(), nd, float(s_clip),
+         *[t.data_ptr() for t in tmp], stream)
+    for t, u in zip(outs, tmp):
+        t[ridx] = u

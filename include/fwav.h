@@ -34,6 +34,9 @@ extern "C" {
 /* ---------------------------------------------------------------------------------------- plumbing */
 const char* fwav_last_error(void);
 int fwav_abi_version(void);
+/* SHA-256 (hex) of the sources and compiler flags this library was built from (__graft_entry__.build writes it in;
+ * fwav/_lib.py refuses a library whose digest differs from the sources beside it). */
+const char* fwav_build_digest(void);
 /* Blocks until `stream` is idle; surfaces asynchronous kernel faults as FWAV_ERR_HIP. */
 int fwav_stream_sync(void* stream);
 
@@ -60,12 +63,18 @@ int fwav_debug_smooth(const float* energy, int64_t nf, int smooth_window, float*
 /* ------------------------------------------------------------------- domain pool + embeddings
  * Replaces build_domains_memmap (fractal.py:285-334) and build_domain_embeddings → multi_head_embedding →
  * tile_embedding / transient_embedding (fractal.py:238-280, 166-208, 154-164).
- * pool f32[n_domains·range_size] (bit-exact), emb f32[n_domains·16] (|Δ| ≤ 1e-6 vs the reference),
+ * pool f32[n_domains·range_size] (bit-exact), emb f32[n_domains·16] (bit-exact for range_size 4, 8, 16: scipy's own
+ * pocketfft DCT sequence in f32 and f64 and numpy's BLAS norm orders; |Δ| ≤ 1e-6 for other range sizes),
  * emb16 (optional) fp16 copies in the search's tiled layout, f16[fwav_emb16_elems(n_domains)]: the high part
  * f16(emb) then the low part f16(emb − f16(emb)), ceil(n_domains/256)·256·16 halfs each.
- * n_domains = (n − tile) / step + 1.  tab = device copy of fwav_embed_tables(range_size) (host call). */
+ * n_domains = (n − tile) / step + 1.  tab = device copy of fwav_embed_tables(range_size) (host call, tab_host holds
+ * fwav_embed_tables_size(range_size) doubles). */
 size_t fwav_emb16_elems(int64_t n_domains);
-int fwav_embed_tables(int range_size, double* tab_host /* [16·range_size] */);
+size_t fwav_embed_tables_size(int range_size);
+int fwav_embed_tables(int range_size, double* tab_host);
+/* Test hook (host, no device): scipy.fftpack.dct(x, norm='ortho') for n = 4, 8, 16 in float32 (dbl = 0) or float64
+ * through the embedding kernel's own code (x and out are doubles). */
+int fwav_debug_dct2(int n, int dbl, const double* x, double* out);
 size_t fwav_pool_workspace_size(int64_t n, int tile, int range_size, int step);
 int fwav_pool_embed(const float* sig, int64_t n, int tile, int range_size, int step, const double* tab, float* pool,
                     float* emb, void* emb16, void* workspace, size_t ws_bytes, void* stream);
@@ -85,9 +94,12 @@ int fwav_prune(const float* ranges, int64_t n, int64_t q_offset, int range_size,
 /* ------------------------------------------------------------------- similarity top-K
  * Replaces range_candidates_from_embedding_emb + pad_candidates (fractal.py:535-552, 617-622): for each
  * local query listed in active[0 .. *n_active) (at most max_q entries; max_q bounds their number, not their
- * values — a listed i only needs its cand row), the K domains with the largest f32 score
- * fma_k(emb[d][k]·emb[q_offset+i][k]) in (score desc, index asc) order, −1-padded when n_domains < K,
- * into cand[i·K .. i·K+K).  K ≤ 64: emb16 != NULL selects the fp16 MFMA pre-filter + exact f32 rescoring
+ * values — a listed i only needs its cand row), the K domains with the largest f32 score emb[d]·emb[q_offset+i]
+ * evaluated in the reference's own BLAS order (OpenBLAS sgemv_t over `blas_threads` threads: the thread split
+ * decides which columns its tail kernels score; fwav_common.h), in (score desc, index asc) order, −1-padded when
+ * n_domains < K, into cand[i·K .. i·K+K).  ties (device int32[1 + max_q], may be NULL): ties[0] = the number of
+ * queries whose top K + 1 scores hold exactly equal values, ties[1 + j] = 2·i + (1 if the K-th and (K+1)-th are
+ * equal) — rows whose order (or set) the reference leaves to numpy's argpartition/argsort; see fwav_tie_check.  K ≤ 64: emb16 != NULL selects the fp16 MFMA pre-filter + exact f32 rescoring
  * kernel, emb16 == NULL the all-f32 MFMA kernel; both return identical candidates.  K > 64 (the module-global
  * top_k is unrestricted in the reference; K ≥ n_domains returns every domain sorted): batched exact score
  * rows + per-query select and sort (fwav_topk_large.hip).  `workspace` holds
@@ -96,8 +108,13 @@ int fwav_prune(const float* ranges, int64_t n, int64_t q_offset, int range_size,
 int fwav_topk_max_k(void);
 size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k);
 int fwav_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
-                  const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand, void* workspace,
-                  size_t ws_bytes, void* stream);
+                  const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int blas_threads, int32_t* cand,
+                  int32_t* ties, void* workspace, size_t ws_bytes, void* stream);
+/* Exact reference score rows (for resolving ties on the host with numpy's own calls): scores[i·n_domains + d] =
+ * emb[d]·emb[q_offset + rows[i]] in the order of fwav_sim_topk, i < n_rows (device f32[n_rows·n_domains]).
+ * Replaces `scores = domain_embs @ q` (fractal.py:537). */
+int fwav_score_rows(const float* emb, int64_t n_domains, const int32_t* rows, int64_t n_rows, int64_t q_offset,
+                    int blas_threads, float* scores, void* stream);
 /* Diagnostic ablations of the fp16 kernel (timing only, outputs invalid for dbg & 65535 != 0); stats (u64[16]
  * device, may be NULL) receives slow-path counters — of the first pass, or with dbg = 1 << 17 of the exact-mode
  * relaunch for overflowed queries only (outputs valid).  Not used by the product path. */
@@ -129,6 +146,14 @@ int fwav_debug_topk_geometry(int wide);
 int fwav_affine(const float* ranges, int64_t n_ranges, int range_size, const int32_t* cand, int k, const float* pool,
                 int64_t n_domains, float s_clip, int32_t* out_idx, float* out_s, float* out_o, uint8_t* out_sym,
                 float* out_err, void* stream);
+/* Tie check (after fwav_affine on the same rows): for every query listed in ties (fwav_sim_topk), decide whether the
+ * reference's numpy tie order could change its match — a tie at the K-th place always can; equal scores inside the
+ * top K only when two candidates of one run of equal scores both attain the minimum error (fractal.py:816-824).
+ * resolve (device int32[1 + max_ties]): resolve[0] = count, resolve[1 + j] = local row to resolve on the host
+ * (fwav.ties.resolve_rows: exact score rows, numpy's argpartition/argsort, fwav_affine on those rows). */
+int fwav_tie_check(const float* ranges, int64_t n_ranges, int range_size, const int32_t* cand, int k,
+                   const float* pool, int64_t n_domains, const float* emb, int64_t q_offset, int blas_threads,
+                   const int32_t* ties, int64_t max_ties, int32_t* resolve, void* stream);
 /* Diagnostic (bench roofline, not the product path): n uniformly random rows of rs floats (rs 4/8/16, 16-B aligned
  * table of n_rows rows) gathered with nothing computed — the ceiling of fwav_affine's memory side on this device.
  * sink: one float of device memory. */

@@ -66,12 +66,15 @@ def pw_mean(x: np.ndarray) -> np.ndarray:
     return pw_sum(x) / F32(x.shape[-1])
 
 
-def seq_dot_f32(a: np.ndarray, b: np.ndarray) -> np.ndarray:
-    """Short BLAS sdot (n < 32 → OpenBLAS tail loop): sequential float32 accumulation, rows batched."""
-    acc = np.zeros(a.shape[:-1], F32)
+def sdot_f32(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Short BLAS sdot, as np.linalg.norm of a 1-D float32 vector evaluates it (fractal.py:205 ``sqrt(e.dot(e))``):
+    OpenBLAS's x86_64 sdot runs n < 32 entirely in its tail loop, ``double dot += (float)(y[i] * x[i])`` — each
+    product rounded to float32, accumulated in float64 in index order, the sum rounded to float32 on return.
+    Measured bit-exact against numpy (OpenBLAS 0.3.29) on every golden embedding row; rows batched."""
+    acc = np.zeros(a.shape[:-1], np.float64)
     for i in range(a.shape[-1]):
-        acc = acc + a[..., i] * b[..., i]
-    return acc
+        acc = acc + (a[..., i] * b[..., i]).astype(np.float64)
+    return acc.astype(F32)
 
 
 def seq_dot_f64(a: np.ndarray, b: np.ndarray) -> np.ndarray:
@@ -220,7 +223,7 @@ def embed(pool: np.ndarray, emb_dim: int = 16) -> np.ndarray:
     take = min(tk, max(0, n - 1))
     e = np.zeros((nd, tk), F32)
     e[:, :take] = v[:, 1:1 + take].astype(F32)
-    nrm = np.sqrt(seq_dot_f32(e, e))
+    nrm = np.sqrt(sdot_f32(e, e))
     ok = nrm > F32(1e-8)
     e[ok] = e[ok] / nrm[ok, None]
     d = np.diff(pool, axis=-1, prepend=pool[:, :1]) * w
@@ -240,10 +243,11 @@ def range_energy_pruned(ranges: np.ndarray, energy_thresh: float, fast_mode: boo
     return pw_mean(ranges * ranges) < prune_threshold(energy_thresh)
 
 
-def zero_query_candidates(nd: int, k: int) -> np.ndarray:
-    """range_candidates_from_embedding_emb (fractal.py:535-541) + pad_candidates (:544-552) for an all-zero query
-    (quirk Q11): every score is 0, so the row is the order numpy's argpartition/argsort leave equal keys in."""
-    scores = np.zeros(nd, F32)
+def numpy_topk_row(scores: np.ndarray, k: int) -> np.ndarray:
+    """range_candidates_from_embedding_emb (fractal.py:535-541) + pad_candidates (:544-552) on one score row, by the
+    same numpy calls: argpartition(scores, −K)[−K:] ordered by argsort(...)[::-1] (a full argsort when K ≥ nd), −1
+    padded to K.  Exactly equal scores come out in the order numpy's selection and sort leave them."""
+    nd = len(scores)
     if k >= nd:
         idx = np.argsort(scores)[::-1]
     else:
@@ -254,22 +258,74 @@ def zero_query_candidates(nd: int, k: int) -> np.ndarray:
     return out
 
 
-def sgemv_scores(emb: np.ndarray, q: np.ndarray) -> np.ndarray:
+def zero_query_candidates(nd: int, k: int) -> np.ndarray:
+    """The row of an all-zero query (quirk Q11): every score is 0, so numpy's tie order decides the whole row."""
+    return numpy_topk_row(np.zeros(nd, F32), k)
+
+
+def blas_threads() -> int:
+    """OpenBLAS's thread count in this process (what numpy's sgemv would split over; sgemv_col_kind)."""
+    try:
+        import threadpoolctl
+        for info in threadpoolctl.threadpool_info():
+            if info.get("user_api") == "blas":
+                return int(info["num_threads"])
+    except Exception:
+        pass
+    import os
+    return os.cpu_count() or 1
+
+
+#: OpenBLAS (interface/gemv.c) runs sgemv single-threaded while m·n < 115200·GEMM_MULTITHREAD_THRESHOLD (= 4)
+SGEMV_THREAD_MIN_MN = 460_800
+
+
+def sgemv_col_kind(cols, nd: int, threads: int) -> np.ndarray:
+    """Which OpenBLAS sgemv_t kernel scores column (domain) d of the reference's ``domain_embs @ q`` (fractal.py:537):
+    0 = the 4-column microkernel, 1 = the 4x2 tail kernel, 2 = the 4x1 tail kernel.  gemv_thread.c splits the nd
+    columns over T threads (T = 1 while 16·nd < SGEMV_THREAD_MIN_MN, else OpenBLAS's thread count) in widths
+    ceil(rest / threads left) — the first nd mod T chunks one column wider — and each thread's sgemv_t scores its
+    chunk's last (width mod 4) columns with the tail kernels (2 → 4x2, 1 → 4x1, 3 → 4x2 then 4x1).  Pinned against
+    numpy here for T = 1, 3, 5, 7, 8 and nd from 577 to 6.6 M (every column bit-exact)."""
+    d = np.asarray(cols, np.int64)
+    T = 1 if 16 * nd < SGEMV_THREAD_MIN_MN else max(1, int(threads))
+    q, r = divmod(int(nd), T)
+    big = d < r * (q + 1)
+    w = np.where(big, q + 1, q)
+    start = np.where(big, d // (q + 1) * (q + 1), r * (q + 1) + (d - r * (q + 1)) // max(q, 1) * q)
+    pos = d - start
+    t = w & 3
+    body = pos < w - t
+    two = ((t & 2) != 0) & (pos < w - t + 2)
+    return np.where(body, 0, np.where(two, 1, 2)).astype(np.int8)
+
+
+def sgemv_scores(emb: np.ndarray, q: np.ndarray, kinds=None) -> np.ndarray:
     """emb @ q for a block of queries q (R, 16), in the order the reference's BLAS evaluates it (fractal.py:537:
-    numpy sgemv → OpenBLAS sgemv_t 4-column microkernel): l_j = fma(d[j+8], q[j+8], f32(d[j]·q[j])), then
-    ((l0 + l4) + (l1 + l5)) + ((l2 + l6) + (l3 + l7)).  The fma is evaluated in x87 extended precision (the 48-bit
-    product is exact; the one further rounding before f32 is a double rounding only at an exact extended-precision
-    midpoint).  Bit-exact against numpy here except the table's last n_domains mod 4 columns (OpenBLAS's tail
-    kernel).  Returns (R, nd) float32."""
+    numpy sgemv → OpenBLAS 0.3.29 sgemv_t, Haswell/SkylakeX kernels), per column kind (sgemv_col_kind; None = all 0):
+      0: 8 fma lanes l_j = fma(d[j+8], q[j+8], 0 + d[j]·q[j]), then ((l0 + l4) + (l1 + l5)) + ((l2 + l6) + (l3 + l7));
+      1: 4 SSE lanes l_j = ((0 + p_j) + p_{j+4}) + p_{j+8}) + p_{j+12} of rounded products p, then (l0 + l1) + (l2 + l3);
+      2: 8 lanes l_j = (0 + p_j) + p_{j+8}, then ((l0 + l4) + (l1 + l5)) + ((l2 + l6) + (l3 + l7)).
+    Bit-exact against numpy on every column (sgemv_col_kind).  Returns (R, n) float32."""
     E = np.asarray(emb, F32)
     Q = np.asarray(q, F32)
+    P = [Q[:, None, j] * E[None, :, j] for j in range(16)]          # rounded f32 products
+    z = F32(0)
     lanes = []
     for j in range(8):
-        c = Q[:, None, j] * E[None, :, j]                       # f32 product, rounded
         p = Q[:, None, j + 8].astype(np.float64) * E[None, :, j + 8].astype(np.float64)  # exact
-        lanes.append(fma_f32(p, c.astype(np.float64)))
+        lanes.append(fma_f32(p, (z + P[j]).astype(np.float64)))
     r = [lanes[i] + lanes[i + 4] for i in range(4)]
-    return (r[0] + r[1]) + (r[2] + r[3])
+    out = (r[0] + r[1]) + (r[2] + r[3])
+    if kinds is None or not np.any(kinds):
+        return out
+    kinds = np.asarray(kinds)
+    l4 = [(((z + P[j]) + P[j + 4]) + P[j + 8]) + P[j + 12] for j in range(4)]
+    a = (l4[0] + l4[1]) + (l4[2] + l4[3])
+    l8 = [(z + P[j]) + P[j + 8] for j in range(8)]
+    r8 = [l8[i] + l8[i + 4] for i in range(4)]
+    b = (r8[0] + r8[1]) + (r8[2] + r8[3])
+    return np.where(kinds[None, :] == 1, a, np.where(kinds[None, :] == 2, b, out))
 
 
 def fma_f32(p: np.ndarray, c: np.ndarray) -> np.ndarray:
@@ -297,13 +353,17 @@ def fma_f32(p: np.ndarray, c: np.ndarray) -> np.ndarray:
 SGEMV_GAP = 8e-6
 
 
-def topk_candidates(emb: np.ndarray, n_ranges: int, k: int, pruned: np.ndarray, chunk: int = 512):
+def topk_candidates(emb: np.ndarray, n_ranges: int, k: int, pruned: np.ndarray, chunk: int = 512,
+                    threads: int | None = None, stats: dict | None = None):
     """cpu_worker + range_candidates_from_embedding_emb + pad_candidates (fractal.py:556-632, 535-552).
     Query for range i is domain-embedding row i (quirk Q1, fractal.py:1190-1195).  Scores in float32 in the
-    reference's sgemv order (sgemv_scores); ties broken by lower index, except all-zero queries, whose row is the
-    reference's own tie order (zero_query_candidates, quirk Q11).
-    Returns (cand i32[nr, k] −1-padded, kth f32[nr], k1th f32[nr])."""
+    reference's sgemv order (sgemv_scores, column kinds for `threads` OpenBLAS threads; default: this process's).
+    Rows whose top K + 1 scores are all distinct are decided by the scores alone (score desc; the K-th beats the
+    (K+1)-th); a row with exactly equal scores among its top K + 1 — and every all-zero query (quirk Q11) — is
+    scored in full and handed to numpy's own argpartition/argsort (numpy_topk_row), whose tie order the reference
+    inherits.  Returns (cand i32[nr, k] −1-padded, kth f32[nr], k1th f32[nr]); stats['ties'] counts tied rows."""
     nd = emb.shape[0]
+    threads = blas_threads() if threads is None else int(threads)
     cand = np.full((n_ranges, k), -1, np.int32)
     kth = np.full(n_ranges, np.nan, F32)
     k1th = np.full(n_ranges, np.nan, F32)
@@ -315,27 +375,35 @@ def topk_candidates(emb: np.ndarray, n_ranges: int, k: int, pruned: np.ndarray, 
     act = np.nonzero(~pruned[:n_ranges] & ~zero)[0]
     kk = min(k, nd)
     E = np.asarray(emb, F32)
+    kind_all = None
+    n_ties = 0
     for s in range(0, len(act), chunk):
         rows = act[s:s + chunk]
         # BLAS scores (another summation order: within SGEMV_GAP of the sgemv order) pick a superset of every
-        # domain that can be in the exact top K; the superset is then scored in the sgemv order and selected exactly
+        # domain that can be in the exact top K + 1; the superset is then scored in the sgemv order and selected exactly
         fast = E[rows] @ E.T
         if kk < nd:
-            Tf = -np.partition(-fast, kk - 1, axis=1)[:, kk - 1]
+            part = -np.partition(-fast, kk, axis=1)
+            Tf = part[:, kk]      # the (K+1)-th BLAS score
         else:
             Tf = fast.min(axis=1)
         for j, r in enumerate(rows):
             sup = np.nonzero(fast[j] >= Tf[j] - SGEMV_GAP)[0]
-            ex = sgemv_scores(E[sup], E[r][None, :])[0]
+            ex = sgemv_scores(E[sup], E[r][None, :], sgemv_col_kind(sup, nd, threads))[0]
             o = np.lexsort((sup, -ex))  # (score desc, index asc)
-            cand[r, :kk] = sup[o[:kk]]
+            top = ex[o[:kk + 1]]
+            if np.any(top[1:] == top[:-1]):
+                n_ties += 1
+                if kind_all is None:
+                    kind_all = sgemv_col_kind(np.arange(nd), nd, threads)
+                cand[r] = numpy_topk_row(sgemv_scores(E, E[r][None, :], kind_all)[0], k)
+            else:
+                cand[r, :kk] = sup[o[:kk]]
             kth[r] = ex[o[kk - 1]]
             if kk < nd:
-                if len(sup) > kk:
-                    k1th[r] = ex[o[kk]]
-                else:  # the (K+1)-th lies more than SGEMV_GAP below: its BLAS score is near enough for a gap test
-                    below = fast[j][fast[j] < Tf[j] - SGEMV_GAP]
-                    k1th[r] = below.max()
+                k1th[r] = ex[o[kk]]
+    if stats is not None:
+        stats["ties"] = n_ties
     return cand, kth, k1th
 
 
@@ -451,7 +519,7 @@ def fwav_bytes(idx, s, o, sym, err, pool, range_size, framerate, sampwidth, tile
 
 
 # ------------------------------------------------------------------------------------- pipeline
-def compress(signal, tile_size, top_k, energy_thresh=1e-4, fast_mode=True):
+def compress(signal, tile_size, top_k, energy_thresh=1e-4, fast_mode=True, threads=None):
     """compress_audio (fractal.py:1045-1256) without the process pipeline.  Returns a dict of stages."""
     signal = np.asarray(signal, F32)
     rs, step = geometry(tile_size)
@@ -460,7 +528,7 @@ def compress(signal, tile_size, top_k, energy_thresh=1e-4, fast_mode=True):
     pool = domain_pool(signal, tile_size, rs, step)
     emb = embed(pool)
     pruned = range_energy_pruned(ranges, energy_thresh, fast_mode)
-    cand, kth, k1th = topk_candidates(emb, len(ranges), top_k, pruned)
+    cand, kth, k1th = topk_candidates(emb, len(ranges), top_k, pruned, threads=threads)
     idx, s, o, sym, err = affine(ranges, cand, pool)
     return dict(rs=rs, step=step, voiced=vm, ranges=ranges, original_len=orig, pool=pool, emb=emb,
                 pruned=pruned, cand=cand, kth=kth, k1th=k1th, idx=idx, s=s, o=o, sym=sym, err=err)

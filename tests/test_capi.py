@@ -46,19 +46,51 @@ def test_bindings_match_header(lib):
 
 def test_error_codes_without_gpu(lib):
     L = lib.lib()
-    assert L.fwav_abi_version() == 2
+    assert L.fwav_abi_version() == 3
     rc = L.fwav_affine(None, 10, 8, None, 64, None, 100, 16.0, None, None, None, None, None, None)
     assert rc == -1 and b"null" in L.fwav_last_error()
-    rc = L.fwav_sim_topk(None, None, 10, None, None, 10, 0, 64, None, None, 0, None)
+    rc = L.fwav_sim_topk(None, None, 10, None, None, 10, 0, 64, 1, None, None, None, 0, None)
     assert rc == -1
     big = ctypes.c_void_p(16)
-    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, L.fwav_topk_max_k() + 1, big, None, 0, None)
+    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 64, 0, big, None, None, 0, None)
+    assert rc == -1 and b"blas_threads" in L.fwav_last_error()
+    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, L.fwav_topk_max_k() + 1, 1, big, None, None, 0, None)
     assert rc == -3 and b"K=" in L.fwav_last_error()
-    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 0, big, None, 0, None)
+    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 0, 1, big, None, None, 0, None)
     assert rc == -3
     # K > 64 needs the score-row workspace
-    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 100, big, None, 0, None)
+    rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 100, 1, big, None, None, 0, None)
     assert rc == -5 and b"workspace" in L.fwav_last_error()
+    rc = L.fwav_tie_check(None, 10, 8, None, 64, None, 100, None, 0, 1, None, 10, None, None)
+    assert rc == -1
+    rc = L.fwav_score_rows(None, 100, None, 1, 0, 1, None, None)
+    assert rc == -1
+
+
+def test_library_digest_matches_sources(lib):
+    """The library reports the digest of the sources and flags it was built from, and it is this tree's
+    (fwav._lib refuses to bind a library built from anything else)."""
+    from fwav import _digest
+    assert lib.lib().fwav_build_digest().decode() == _digest.source_digest()
+
+
+@pytest.mark.parametrize("dbl", [0, 1])
+@pytest.mark.parametrize("n", [4, 8, 16])
+def test_dct_is_scipy_bitexact(lib, n, dbl):
+    """fwav_dct.h (the embedding kernel's DCT, instantiated on the host): scipy.fftpack.dct(x, norm='ortho') bit for
+    bit in float32 (the tonal head, fractal.py:186) and float64 (the transient head, fractal.py:158)."""
+    import scipy.fftpack
+    L = lib.lib()
+    T = np.float64 if dbl else np.float32
+    rng = np.random.default_rng(n + 100 * dbl)
+    out = np.zeros(n)
+    for _ in range(4000):
+        x = (rng.standard_normal(n) * rng.choice([1e-30, 1e-6, 1e-3, 1.0, 1e4])).astype(T)
+        if rng.random() < 0.05:
+            x[rng.integers(n)] = 0
+        xin = x.astype(np.float64)
+        assert L.fwav_debug_dct2(n, dbl, xin.ctypes.data, out.ctypes.data) == 0
+        assert np.array_equal(out.astype(T).view(np.uint8), scipy.fftpack.dct(x, norm="ortho").view(np.uint8)), x
 
 
 def test_embed_tables_match_scipy_dct(lib):
@@ -66,14 +98,14 @@ def test_embed_tables_match_scipy_dct(lib):
     import scipy.fftpack
     L = lib.lib()
     for rs in (4, 8, 16, 13):
-        tab = np.zeros(16 * rs)
+        tab = np.zeros(L.fwav_embed_tables_size(rs))
         assert L.fwav_embed_tables(rs, tab.ctypes.data) == 0
         eye = np.eye(rs)
         D = scipy.fftpack.dct(eye, norm="ortho", axis=0)  # D[k, n]
         w = np.linspace(1.0, 2.0, rs)
         take, tk = min(8, rs - 1), min(8, rs)
         ton = tab[:8 * rs].reshape(8, rs)
-        tra = tab[8 * rs:].reshape(8, rs)
+        tra = tab[8 * rs:16 * rs].reshape(8, rs)
         np.testing.assert_allclose(ton[:take], D[1:1 + take] * w[1:1 + take, None], atol=1e-14)
         np.testing.assert_allclose(tra[:tk], D[:tk] * w[None, :], atol=1e-14)
         assert np.all(ton[take:] == 0) and np.all(tra[tk:] == 0)

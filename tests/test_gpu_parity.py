@@ -1,13 +1,14 @@
 """GPU parity: the HIP path (through the C-ABI) against the reference goldens and the oracle.
 
-Bars: ranges / pool / affine / decode bit-exact; embeddings |Δ| <= 1e-6; candidate
-sets equal except near-ties (golden K-th vs (K+1)-th score gap <= 1e-5) and all-zero queries; end-to-end
-(idx, sym) bit-exact wherever the candidate set matched, s/o/err bit-exact there too.
+Bars: the whole compress bit-exact with the reference on every golden case — ranges, voiced mask, pool, embeddings
+(scipy's own pocketfft sequence), candidate sets (the reference's BLAS score order, numpy's order among exactly tied
+scores wherever it can change a match), every (domain_index, s, o, symmetry_flag, err) tuple, the .fwav bytes — and
+the decode bit-exact.
 """
 import numpy as np
 import pytest
 
-from golden_util import CASES, GPU_MATCH_FLOOR, GPU_TIE_GAP, bit_equal, candidate_agreement, load, match_agreement
+from golden_util import CASES, bit_equal, load
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -40,37 +41,34 @@ def test_ranges_pool_embed(case):
     assert bit_equal(r.ranges.cpu().numpy().reshape(-1, rs), g["ranges"])
     assert bit_equal(r.pool.cpu().numpy().reshape(-1, rs), g["pool"])
     emb = r.emb.cpu().numpy().reshape(-1, 16)
-    assert np.abs(emb - g["emb"]).max() <= 1e-6
+    assert bit_equal(emb, g["emb"])
 
 
 @pytest.mark.parametrize("case", CASES)
 def test_candidates_and_matches(case):
-    """Rule 3 on the candidate sets (all-zero queries included: they reproduce the reference's introselect order,
-    quirk Q11), rule 4 on every range's (idx, sym), bit-exact s/o/err wherever (idx, sym) agree, and the measured
-    agreement rate held at its floor."""
+    """The reference's candidate set for every range and its order wherever the top-K scores are distinct (among
+    exactly equal scores the device keeps index order unless numpy's order can change the match — fwav.ties), and
+    every match tuple bit-exact (SURVEY Appendix A rules 3-4 at their strictest: no exceptions)."""
+    from oracle import fractal_oracle as O
     g = load(case)
     p = g["p"]
     for K in p["Ks"]:  # includes ragged K=2000 >= n_domains (full sort, −1 padded)
         r = run_case(g, K)
         cand = r.cand.cpu().numpy().reshape(-1, K)
         gold = g[f"cand_{K}"]
-        pruned = gold[:, 0] < 0
-        # pruned rows identical (all −1)
-        assert np.array_equal(cand[pruned], gold[pruned])
-        zeroq = np.all(g["emb"][:len(cand)] == 0, axis=1) & ~pruned
-        assert np.array_equal(cand[zeroq], gold[zeroq]), f"{case} K={K}: Q11 rows differ from the reference"
-        same, bad = candidate_agreement(cand, gold, g[f"kth_{K}"], g[f"k1th_{K}"], None, pruned, gap=GPU_TIE_GAP)
-        assert not bad.any(), f"{case} K={K}: {bad.sum()} unexplained candidate-set mismatches"
-        idx, sym, err = (t.cpu().numpy() for t in (r.idx, r.sym, r.err))
-        exact, equal_fit, near, unexplained = match_agreement(idx, sym, err, g, K, gap=GPU_TIE_GAP)
-        assert not unexplained.any(), f"{case} K={K}: {unexplained.sum()} (idx, sym) mismatches break rule 4"
-        for nm, t in (("s", r.s), ("o", r.o), ("err", r.err)):
-            assert bit_equal(t.cpu().numpy()[exact], g[f"m_{nm}_{K}"][exact]), f"{case} K={K} {nm}"
-        rate = exact.mean()
-        print(f"{case} K={K}: candidate sets equal {same.mean():.4f}, (idx, sym) equal {rate:.4f}, "
-              f"mismatches {(~exact).sum()}: equal fit {(~exact & equal_fit).sum()}, near-tie "
-              f"{(~exact & ~equal_fit & near).sum()}")
-        assert rate >= GPU_MATCH_FLOOR[(case, K)], f"{case} K={K}: (idx, sym) agreement {rate:.4f}"
+        assert all(set(a.tolist()) == set(b.tolist()) for a, b in zip(cand, gold)), f"{case} K={K}: candidate sets"
+        # order: equal wherever the golden row's scores are all distinct
+        emb = g["emb"]
+        for i in range(len(gold)):
+            c = gold[i][gold[i] >= 0]
+            if len(c) == 0:
+                continue
+            sc = O.sgemv_scores(emb[c], emb[i][None, :], O.sgemv_col_kind(c, len(emb), 8))[0]
+            if len(np.unique(sc)) == len(sc):
+                assert np.array_equal(cand[i], gold[i]), f"{case} K={K} row {i}"
+        for nm, t in (("idx", r.idx), ("s", r.s), ("o", r.o), ("sym", r.sym), ("err", r.err)):
+            assert bit_equal(t.cpu().numpy(), g[f"m_{nm}_{K}"]), f"{case} K={K} {nm}"
+        print(f"{case} K={K}: {r.n_ties} rows with exact ties, {r.n_resolved} re-ranked by numpy; all tuples exact")
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -136,17 +134,10 @@ def test_reference_e2e_tone(tmp_path):
     # body, pool, 17-byte match records): header and pool always; every match record but those of the tone's
     # byte-identical-tile ranges (equal fits, rule 4), whose (idx, sym) follow a different tie order — and with
     # them the digest
-    from oracle.fractal_oracle import HEADER_SIZE
-    mine, ref = np.frombuffer(fw.read_bytes(), np.uint8), g["fwav_32"]
-    assert len(mine) == len(ref)
-    ex = (np.asarray(matches.idx) == g["m_idx_32"]) & (np.asarray(matches.sym) == g["m_sym_32"])
-    pool_end = HEADER_SIZE + 32 + domains.size * 4
-    assert np.array_equal(mine[:HEADER_SIZE], ref[:HEADER_SIZE])
-    assert np.array_equal(mine[HEADER_SIZE + 32:pool_end], ref[HEADER_SIZE + 32:pool_end])
-    mrec, rrec = mine[pool_end:].reshape(-1, 17), ref[pool_end:].reshape(-1, 17)
-    assert np.array_equal(mrec[ex], rrec[ex])
-    if ex.all():
-        assert np.array_equal(mine, ref)
+    # the .fwav written here is the reference's file byte for byte (fractal.py:1278-1322: header, SHA-256 of the
+    # body, pool, 17-byte match records) — the tone's byte-identical tiles included, whose matches follow numpy's
+    # order among exactly tied scores
+    assert np.array_equal(np.frombuffer(fw.read_bytes(), np.uint8), g["fwav_32"])
 
 
 def _cands(sig, tile, K, search, thr=1e-4):
@@ -236,6 +227,8 @@ def test_large_k_prefix_equals_k64(gen, tile):
 
 @pytest.mark.parametrize("K", [65, 300, 1000])
 def test_large_k_vs_oracle(K):
+    """K > 64 (batched score rows + select): candidate sets equal the oracle's (the reference's numpy calls on the
+    reference-order scores) for every range, and every match tuple equals the oracle's."""
     from oracle import fractal_oracle as orc
 
     g = load("noise2048")
@@ -243,9 +236,11 @@ def test_large_k_vs_oracle(K):
     r = run_case(g, K)
     cand = r.cand.cpu().numpy().reshape(-1, K)
     pruned = cand[:, 0] < 0
-    ocand, kth, k1th = orc.topk_candidates(g["emb"], p["n_ranges"], K, pruned)
-    same, bad = candidate_agreement(cand, ocand, kth, k1th, g["emb"][:len(cand)], pruned)
-    assert not bad.any(), f"K={K}: {bad.sum()} unexplained mismatches"
+    ocand, _, _ = orc.topk_candidates(g["emb"], p["n_ranges"], K, pruned, threads=8)
+    assert all(set(a.tolist()) == set(b.tolist()) for a, b in zip(cand, ocand))
+    out = orc.affine(g["ranges"], ocand, g["pool"])
+    for t, b in zip((r.idx, r.s, r.o, r.sym, r.err), out):
+        assert bit_equal(t.cpu().numpy(), np.asarray(b))
 
 
 @pytest.mark.parametrize("wide", [0, 1], ids=["base", "wide"])
@@ -299,8 +294,8 @@ def test_overflow_with_sparse_active_list(first_mode):
         guard = 1 << 20
         wsk = torch.zeros(wsn + guard, dtype=torch.uint8, device=sig.device)
         cand = torch.full((n * K,), -7, dtype=torch.int32, device=sig.device)
-        call("fwav_sim_topk", emb.data_ptr(), e16, nd, rows.data_ptr(), n_act.data_ptr(), max_q, 0, K,
-             cand.data_ptr(), wsk.data_ptr(), wsn, st)
+        call("fwav_sim_topk", emb.data_ptr(), e16, nd, rows.data_ptr(), n_act.data_ptr(), max_q, 0, K, 1,
+             cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
         torch.cuda.synchronize()
         assert int(wsk[wsn:].count_nonzero().item()) == 0, "write past the workspace"
         out.append(cand.view(n, K)[rows.long()].cpu().numpy())
