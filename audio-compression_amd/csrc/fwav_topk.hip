@@ -161,7 +161,9 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
   float* lda = (float*)(keys + (size_t)kTopkQ * C);            // [kChunk][16] (row-major domain rows)
   int* cnt = (int*)(lda + 16 * kChunk);                        // [kTopkQ]
   float* theta = (float*)(cnt + kTopkQ);                       // [kTopkQ]
-  int* tieb = (int*)(theta + kTopkQ);                          // [kTopkQ] a domain equal to θ was not kept
+  // [kTopkQ] f2key of the largest θ that a domain of equal score was not kept at (0: none); the set among equal
+  // scores is numpy's choice only if that θ is the final K-th score (θ rises, so earlier ones are superseded)
+  uint32_t* tieb = (uint32_t*)(theta + kTopkQ);
 
   const int n_active = *n_active_p;
   const int qbase = blockIdx.x * kTopkQ;
@@ -248,7 +250,7 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
             const int slot = atomicAdd(&cnt[ql], 1);
             kq[slot] = make_key(acc[r], (int32_t)(d0 + (r & 3) + 8 * (r >> 2)));
           } else if (acc[r] == th && th != -INFINITY) {
-            tieb[ql] = 2;  // equal to the K-th but later in index order: not kept, so the set may be numpy's choice
+            atomicMax(&tieb[ql], f2key(th));  // equal to θ but later in index order: not kept
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -256,7 +258,8 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
         while (need != 0ull) {
           const int l = __builtin_ctzll(need);
           need &= need - 1;
-          if (compact<C>(keys, cnt, theta, wave * 32 + l, K) & 2) tieb[wave * 32 + l] = 2;
+          if ((compact<C>(keys, cnt, theta, wave * 32 + l, K) & 2) && lane == 0)
+            atomicMax(&tieb[wave * 32 + l], f2key(theta[wave * 32 + l]));
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (q >= 0) th = theta[ql];
@@ -271,7 +274,8 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
     if (qq >= n_active) break;
     const int32_t qid = active[qq];
     const int tf = compact<C>(keys, cnt, theta, qs, K);
-    record_tie(ties, qid, tf | tieb[qs]);
+    const uint32_t tv = tieb[qs];
+    record_tie(ties, qid, tf | (tv != 0u && cnt[qs] >= K && key2f(tv) == theta[qs] ? 2 : 0));
     const int n = cnt[qs];
     int32_t* out = cand + (int64_t)qid * K;
     for (int e = lane; e < K; e += 64) out[e] = e < n ? key_idx(keys[(size_t)qs * C + e]) : -1;
@@ -530,7 +534,9 @@ struct Topk16SmemT {
   int cnt[32 * NG];   // final pass: entries at the front of the query's buffer (its h = 0 lane's appends)
   int cnt1[32 * NG];  // ... and at the back (its h = 1 lane's)
   int ovf[32 * NG];  // band overflowed the buffer (f2key of its band limit, else 0): recompute in exact mode
-  int tie[32 * NG];  // exact mode: a domain scoring exactly the K-th score was not kept (tie_flags bit 1)
+  // exact mode: f2key of the largest K-th score that a domain of equal score was not kept at (0: none) — a boundary
+  // tie (tie_flags bit 1) only if it is the final K-th score
+  uint32_t tie[32 * NG];
   int64_t qrow[32 * NG];
   int32_t qpos[32 * NG];  // position of the slot's query in the active list (index of its shared band limit)
   uint32_t fired[NG][kFifo];                       // deferred work: ring of fired chunk entries
@@ -663,7 +669,12 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
   }
   wave_sort_desc<E>(v);
   // exactly tied scores at the top: listed for fwav_tie_check (not for a query about to be searched again)
-  const int tf = tie_flags<E>(v, n, K) | sm.tie[ql];
+  uint64_t kth = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j)
+    if (j == ((K - 1) >> 6)) kth = __shfl(v[j], (K - 1) & 63);
+  const uint32_t tv = sm.tie[ql];
+  const int tf = tie_flags<E>(v, n, K) | (tv != 0u && n >= K && key2f(tv) == key_score(kth) ? 2 : 0);
   if (sm.ovf[ql] == 0) record_tie(ties, qid, tf);
   // Emit straight from registers (never read back what was just stored: a load issued right behind the stores
   // of the same addresses can return the old contents): the K candidate indices, −1-padded.
@@ -754,7 +765,7 @@ __device__ __forceinline__ int fold16(int r, const floatx16& a) {
 // s16 > S32_K − δ: that is the returned filter limit.
 template <int C>
 __device__ __forceinline__ void compact_exact(uint64_t* __restrict__ kq, int n0, int n1, int K, int& m_out,
-                                              float& lim_out, uint64_t& kth_out, int* __restrict__ tie_slot) {
+                                              float& lim_out, uint64_t& kth_out, uint32_t* __restrict__ tie_slot) {
   constexpr int E = C / 64;
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -786,7 +797,7 @@ __device__ __forceinline__ void compact_exact(uint64_t* __restrict__ kq, int n0,
     if (j == kj) kh = (uint32_t)a;
     if (j == kj1) k1h = (uint32_t)b;
   }
-  if (lane == 0 && n > K && key2f(k1h) == key2f(kh)) *tie_slot = 2;
+  if (lane == 0 && n > K && key2f(k1h) == key2f(kh)) atomicMax(tie_slot, kh);
   m_out = n < K ? n : K;
   lim_out = n >= K ? key_score(kth) - kF16Delta : -INFINITY;
   kth_out = n >= K ? kth : 0ull;
@@ -863,7 +874,8 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
             *reinterpret_cast<uint64_t*>(kbase + (uint32_t)((ql * C + slot) * 8)) = k64;
             slot += step;
           } else if (key_score(k64) == key_score(*kthp)) {
-            sm.tie[ql] = 2;  // equal to the K-th exact score, later in index order: numpy decides whether it is in
+            // equal to the K-th exact score, later in index order: numpy decides whether it is in
+            atomicMax(&sm.tie[ql], (uint32_t)(*kthp >> 32));
           }
         }
       }
