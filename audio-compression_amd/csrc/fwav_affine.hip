@@ -335,23 +335,78 @@ __global__ __launch_bounds__(64 * kAffWaves) void k_affine_batch(const float* __
 // [K originals | K mirrors]).  Equal scores occupy one contiguous run of positions in both orders, so a reordering
 // moves candidates only within their run: the first slot that attains the minimum error keeps its candidate unless
 // another candidate of the same run attains it too (originals first; the mirrors only decide when no original
-// does).  Such queries — and every query with a tie at the K-th place, whose set itself is numpy's — go to
-// `resolve` for the host (fwav.ties: exact score rows + numpy's own calls).  One wave per listed query, K ≤ 64
-// (lane c ↔ position c); for K > 64 every listed query is resolved.
+// does).  A tie at the K-th place lets numpy choose which members G of the K-th score's group fill the last places;
+// that cannot change the match when every member of G — the search records the ones left out — fits strictly worse
+// (both orientations) than the best candidate outside G, whose slot is then the minimum whatever the choice.  Queries
+// that fail either test, and K-th place ties whose group the search could not collect (or all of them with
+// exact_sets: the candidate sets themselves are then the reference's), go to `resolve` for the host (fwav.ties:
+// exact score rows + numpy's own calls).  One wave per listed query, K ≤ 64 (lane c ↔ position c); for K > 64 every
+// listed query is resolved.
 __device__ __forceinline__ bool same_err(float a, float b) { return (a != a && b != b) || a == b; }
+
+// Both orientations' errors of tile `di` against range R, exactly as fwav_affine computes them.
+template <int RS>
+__device__ __forceinline__ void pair_errors(const float* __restrict__ R, int rs, const float* __restrict__ pool,
+                                            int32_t di, float& e0, float& e1) {
+  if constexpr (RS > 0) {
+    float Rr[RS], rc[RS], D[RS], M[RS];
+#pragma unroll
+    for (int i = 0; i < RS; ++i) Rr[i] = R[i];
+    auto fr = [&](int i) { return Rr[i]; };
+    const float rm = pw_sum_n<RS>(fr) / (float)RS;
+#pragma unroll
+    for (int i = 0; i < RS; ++i) rc[i] = Rr[i] - rm;
+#pragma unroll
+    for (int i = 0; i < RS; ++i) D[i] = pool[(int64_t)di * RS + i];
+#pragma unroll
+    for (int i = 0; i < RS; ++i) M[i] = D[RS - 1 - i];
+    float s0, o0, s1, o1;
+    eval_orient<RS>(D, Rr, rc, rm, s0, o0, e0);
+    eval_orient<RS>(M, Rr, rc, rm, s1, o1, e1);
+  } else {
+    const int n = rs;
+    auto fr = [&](int i) { return R[i]; };
+    const float rm = pw_sum(fr, n) / (float)n;
+    const float* D = pool + (int64_t)di * n;
+    float ee[2];
+    for (int orient = 0; orient < 2; ++orient) {
+      auto X = [&](int i) { return orient ? D[n - 1 - i] : D[i]; };
+      const float dm = pw_sum(X, n) / (float)n;
+      auto fn = [&](int i) { return (X(i) - dm) * (R[i] - rm); };
+      auto fd = [&](int i) {
+        const float t = X(i) - dm;
+        return t * t;
+      };
+      const float num = pw_sum(fn, n);
+      const float den = pw_sum(fd, n) + 1e-12f;
+      const float s = num / den;
+      const float o = rm - s * dm;
+      auto fe = [&](int i) {
+        const float df = (s * X(i) + o) - R[i];
+        return df * df;
+      };
+      ee[orient] = sqrtf(pw_sum(fe, n));
+    }
+    e0 = ee[0];
+    e1 = ee[1];
+  }
+}
 
 template <int RS>
 __global__ __launch_bounds__(256) void k_tie_check(const float* __restrict__ ranges, int rs,
                                                    const int32_t* __restrict__ cand, int K,
                                                    const float* __restrict__ pool, const float* __restrict__ emb,
                                                    int64_t q_offset, SgemvSplit sp, const int32_t* __restrict__ ties,
-                                                   int32_t* __restrict__ resolve) {
+                                                   int exact_sets, int32_t* __restrict__ resolve) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= ties[0]) return;
-  const int32_t ent = ties[1 + w];
+  const int32_t* rec = ties + 1 + (int64_t)kTieRec * w;
+  const int32_t ent = rec[0];
   const int32_t row = ent >> 1;
-  bool dep = (ent & 1) != 0 || K > 64;
+  const bool boundary = (ent & 1) != 0;
+  const int ng = boundary ? rec[1] : 0;  // tied domains left out of the K (−1: group not collected)
+  bool dep = K > 64 || (boundary && (exact_sets || ng < 0));
   if (!dep) {
     const int n = RS > 0 ? RS : rs;
     const bool has = lane < K;
@@ -365,66 +420,48 @@ __global__ __launch_bounds__(256) void k_tie_check(const float* __restrict__ ran
     const bool start = has && (lane == 0 || prev != sc);
     const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
     const int run = __popcll(__ballot(start) & le);
-    // both orientations' errors, exactly as fwav_affine computes them
     const float* R = ranges + (int64_t)row * n;
     float e0, e1;
-    if constexpr (RS > 0) {
-      float Rr[RS], rc[RS], D[RS], M[RS];
-#pragma unroll
-      for (int i = 0; i < RS; ++i) Rr[i] = R[i];
-      auto fr = [&](int i) { return Rr[i]; };
-      const float rm = pw_sum_n<RS>(fr) / (float)RS;
-#pragma unroll
-      for (int i = 0; i < RS; ++i) rc[i] = Rr[i] - rm;
-#pragma unroll
-      for (int i = 0; i < RS; ++i) D[i] = pool[(int64_t)di * RS + i];
-#pragma unroll
-      for (int i = 0; i < RS; ++i) M[i] = D[RS - 1 - i];
-      float s0, o0, s1, o1;
-      eval_orient<RS>(D, Rr, rc, rm, s0, o0, e0);
-      eval_orient<RS>(M, Rr, rc, rm, s1, o1, e1);
-    } else {
-      auto fr = [&](int i) { return R[i]; };
-      const float rm = pw_sum(fr, n) / (float)n;
-      const float* D = pool + (int64_t)di * n;
-      float ee[2];
-      for (int orient = 0; orient < 2; ++orient) {
-        auto X = [&](int i) { return orient ? D[n - 1 - i] : D[i]; };
-        const float dm = pw_sum(X, n) / (float)n;
-        auto fn = [&](int i) { return (X(i) - dm) * (R[i] - rm); };
-        auto fd = [&](int i) {
-          const float t = X(i) - dm;
-          return t * t;
-        };
-        const float num = pw_sum(fn, n);
-        const float den = pw_sum(fd, n) + 1e-12f;
-        const float s = num / den;
-        const float o = rm - s * dm;
-        auto fe = [&](int i) {
-          const float df = (s * X(i) + o) - R[i];
-          return df * df;
-        };
-        ee[orient] = sqrtf(pw_sum(fe, n));
-      }
-      e0 = ee[0];
-      e1 = ee[1];
-    }
+    pair_errors<RS>(R, rs, pool, di, e0, e1);
     if (ci < 0) { e0 = INFINITY; e1 = INFINITY; }
     // the minimum error (first-minimum / NaN-first order of the reference's argmin)
-    float be = has ? e0 : INFINITY;
-    int bs = has ? lane : 0x7fffffff;
-    if (has && better(e1, K + lane, be, bs)) { be = e1; bs = K + lane; }
+    auto arg_min = [&](bool on, float& be, int& bs) {
+      be = on ? e0 : INFINITY;
+      bs = on ? lane : 0x7fffffff;
+      if (on && better(e1, K + lane, be, bs)) { be = e1; bs = K + lane; }
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-      const float oe = __shfl_xor(be, m);
-      const int os = __shfl_xor(bs, m);
-      if (better(oe, os, be, bs)) { be = oe; bs = os; }
+      for (int m = 1; m < 64; m <<= 1) {
+        const float oe = __shfl_xor(be, m);
+        const int os = __shfl_xor(bs, m);
+        if (better(oe, os, be, bs)) { be = oe; bs = os; }
+      }
+    };
+    float be;
+    int bs;
+    arg_min(has, be, bs);
+    if (boundary) {
+      // G = the K-th score's group: its members in the K and the ng left out (rec[2 ..]); each must fit strictly
+      // worse than the best candidate outside G (a NaN error never does)
+      const float S = __shfl(sc, K - 1);
+      const bool in_g = has && sc == S;
+      float bo;
+      int so;
+      arg_min(has && !in_g, bo, so);
+      bool bad = in_g && !(e0 > bo && e1 > bo);
+      if (lane < ng) {
+        float x0, x1;
+        pair_errors<RS>(R, rs, pool, rec[2 + lane], x0, x1);
+        bad = bad || !(x0 > bo && x1 > bo);
+      }
+      dep = __ballot(bad) != 0ull;
     }
-    uint64_t att = __ballot(has && same_err(e0, be));
-    if (att == 0ull) att = __ballot(has && same_err(e1, be));
-    const int first = __builtin_ctzll(att);
-    const int run0 = __shfl(run, first);
-    dep = __popcll(att & __ballot(run == run0)) >= 2;
+    if (!dep) {
+      uint64_t att = __ballot(has && same_err(e0, be));
+      if (att == 0ull) att = __ballot(has && same_err(e1, be));
+      const int first = __builtin_ctzll(att);
+      const int run0 = __shfl(run, first);
+      dep = __popcll(att & __ballot(run == run0)) >= 2;
+    }
   }
   if (dep && lane == 0) {
     const int pos = atomicAdd(resolve, 1);
@@ -479,7 +516,7 @@ int fwav_debug_gather_rows(const float* table, int64_t n_rows, int rs, int64_t n
 
 int fwav_tie_check(const float* ranges, int64_t n_ranges, int rs, const int32_t* cand, int K, const float* pool,
                    int64_t nd, const float* emb, int64_t q_offset, int blas_threads, const int32_t* ties,
-                   int64_t max_ties, int32_t* resolve, void* stream) {
+                   int64_t max_ties, int exact_sets, int32_t* resolve, void* stream) {
   FWAV_CHECK_ARG(ranges && cand && pool && emb && ties && resolve && n_ranges >= 0 && rs >= 1 && K >= 1 && nd >= 1 &&
                      nd < (int64_t)0x7fffffff && max_ties >= 0 && blas_threads >= 1 && blas_threads <= 4096,
                  FWAV_ERR_ARG, "fwav_tie_check: bad args");
@@ -490,10 +527,10 @@ int fwav_tie_check(const float* ranges, int64_t n_ranges, int rs, const int32_t*
   const SgemvSplit sp = make_sgemv_split(nd, blas_threads);
   const int64_t grid = cdiv(max_ties, 4);
   switch (rs) {
-    case 4: k_tie_check<4><<<grid, 256, 0, st>>>(ranges, rs, cand, K, pool, emb, q_offset, sp, ties, resolve); break;
-    case 8: k_tie_check<8><<<grid, 256, 0, st>>>(ranges, rs, cand, K, pool, emb, q_offset, sp, ties, resolve); break;
-    case 16: k_tie_check<16><<<grid, 256, 0, st>>>(ranges, rs, cand, K, pool, emb, q_offset, sp, ties, resolve); break;
-    default: k_tie_check<0><<<grid, 256, 0, st>>>(ranges, rs, cand, K, pool, emb, q_offset, sp, ties, resolve);
+    case 4: k_tie_check<4><<<grid, 256, 0, st>>>(ranges, rs, cand, K, pool, emb, q_offset, sp, ties, exact_sets, resolve); break;
+    case 8: k_tie_check<8><<<grid, 256, 0, st>>>(ranges, rs, cand, K, pool, emb, q_offset, sp, ties, exact_sets, resolve); break;
+    case 16: k_tie_check<16><<<grid, 256, 0, st>>>(ranges, rs, cand, K, pool, emb, q_offset, sp, ties, exact_sets, resolve); break;
+    default: k_tie_check<0><<<grid, 256, 0, st>>>(ranges, rs, cand, K, pool, emb, q_offset, sp, ties, exact_sets, resolve);
   }
   FWAV_LAUNCH_CHECK("fwav_tie_check");
   return FWAV_OK;

@@ -95,6 +95,9 @@ __device__ __forceinline__ auto pw_rec(const F& f, int off, int n) -> decltype(f
 
 // np.add.reduce over n <= kMaxPairwise elements: numpy starts the output at 0 (so -0 sums to +0).
 constexpr int kMaxPairwise = 1024;
+// Records of the search's tie list (fwav_sim_topk `ties`): the query, then its K-th place tie group (fwav_topk.hip
+// record_tie), int32 each.
+constexpr int kTieRec = 9;
 template <class F>
 __device__ __forceinline__ auto pw_sum(const F& f, int n) -> decltype(f(0)) {
   return 0.0f + pw_rec<3>(f, 0, n);

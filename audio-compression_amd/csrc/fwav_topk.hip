@@ -108,12 +108,45 @@ __device__ __forceinline__ int tie_flags(const uint64_t (&v)[E], int n, int K) {
   return (__ballot(in) != 0ull ? 1 : 0) | (__ballot(bd) != 0ull ? 2 : 0);
 }
 
-// Lists query qid for the tie check (fwav_tie_check): ties[0] = count, ties[1 + i] = 2·qid + (boundary tie).
-__device__ __forceinline__ void record_tie(int32_t* ties, int32_t qid, int flags) {
-  if (ties != nullptr && flags != 0 && (threadIdx.x & 63) == 0) {
-    const int pos = atomicAdd(ties, 1);
-    ties[1 + pos] = 2 * qid + ((flags >> 1) & 1);
+// Lists query qid for the tie check (fwav_tie_check): ties[0] = count; record i = ties[1 + kTieRec·i ..]:
+// [0] = 2·qid + (boundary tie), and for a boundary tie [1] = the number of domains outside the emitted K whose score
+// equals the K-th (−1: not known), [2 ..] = those domains.  `v` (sorted, n valid entries) is the query's final band:
+// when `group` is set it holds every domain scoring at least the K-th score, so the tie group is complete.  Whole
+// wave (wave-uniform arguments).
+template <int E>
+__device__ __forceinline__ void record_tie(int32_t* ties, int32_t qid, int flags, const uint64_t (&v)[E], int n,
+                                           int K, bool group) {
+  if (ties == nullptr || flags == 0) return;
+  const int lane = threadIdx.x & 63;
+  int pos = 0;
+  if (lane == 0) pos = atomicAdd(ties, 1);
+  pos = __shfl(pos, 0);
+  int32_t* rec = ties + 1 + (int64_t)kTieRec * pos;
+  if (lane == 0) rec[0] = 2 * qid + ((flags >> 1) & 1);
+  if (!(flags & 2)) return;
+  int total = -1;
+  if (group) {
+    uint64_t kth = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (j == ((K - 1) >> 6)) kth = __shfl(v[j], (K - 1) & 63);
+    const float S = key_score(kth);
+    total = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int e = j * 64 + lane;
+      const bool in = e >= K && e < n && key_score(v[j]) == S;  // sorted: positions K, K + 1, … of the group
+      if (in && e - K < kTieRec - 2) rec[2 + e - K] = key_idx(v[j]);
+      total += __popcll(__ballot(in));
+    }
+    if (total > kTieRec - 2) total = -1;
   }
+  if (lane == 0) rec[1] = total;
+}
+template <int E>
+__device__ __forceinline__ void record_tie(int32_t* ties, int32_t qid, int flags, const uint64_t (&v)[E], int n,
+                                           int K) {
+  record_tie<E>(ties, qid, flags, v, n, K, false);
 }
 
 // Sort query ql's buffer, keep the top K, update count and θ; returns tie_flags of the sorted buffer (a (K+1)-th
@@ -275,7 +308,8 @@ __global__ __launch_bounds__(kTopkThreads) void k_sim_topk_f32(const float* __re
     const int32_t qid = active[qq];
     const int tf = compact<C>(keys, cnt, theta, qs, K);
     const uint32_t tv = tieb[qs];
-    record_tie(ties, qid, tf | (tv != 0u && cnt[qs] >= K && key2f(tv) == theta[qs] ? 2 : 0));
+    const uint64_t none[1] = {0ull};
+    record_tie<1>(ties, qid, tf | (tv != 0u && cnt[qs] >= K && key2f(tv) == theta[qs] ? 2 : 0), none, 0, K);
     const int n = cnt[qs];
     int32_t* out = cand + (int64_t)qid * K;
     for (int e = lane; e < K; e += 64) out[e] = e < n ? key_idx(keys[(size_t)qs * C + e]) : -1;
@@ -675,7 +709,9 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
     if (j == ((K - 1) >> 6)) kth = __shfl(v[j], (K - 1) & 63);
   const uint32_t tv = sm.tie[ql];
   const int tf = tie_flags<E>(v, n, K) | (tv != 0u && n >= K && key2f(tv) == key_score(kth) ? 2 : 0);
-  if (sm.ovf[ql] == 0) record_tie(ties, qid, tf);
+  // the band of the S16 / HL modes holds every domain within the band margin of the K-th score, so the K-th's whole
+  // tie group; exact mode keeps only the top K (a tied domain seen later was dropped: tv)
+  if (sm.ovf[ql] == 0) record_tie<E>(ties, qid, tf, v, n, K, tv == 0u);
   // Emit straight from registers (never read back what was just stored: a load issued right behind the stores
   // of the same addresses can return the old contents): the K candidate indices, −1-padded.
 #pragma unroll
@@ -1550,7 +1586,7 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
     }
   }
   wave_sort_desc<E>(v);
-  record_tie(ties, qid, tie_flags<E>(v, mb < C ? mb : C, K));
+  record_tie<E>(ties, qid, tie_flags<E>(v, mb < C ? mb : C, K), v, mb < C ? mb : C, K, true);
   int32_t* out = cand + (int64_t)qid * K;
 #pragma unroll
   for (int j = 0; j < E; ++j) {
@@ -1787,6 +1823,8 @@ using namespace fwav;
 extern "C" {
 
 int fwav_topk_max_k(void) { return 4096; }
+
+int64_t fwav_tie_list_size(int64_t max_q) { return 1 + (int64_t)kTieRec * (max_q > 0 ? max_q : 1); }
 
 // Workspace of fwav_sim_topk: for K <= 64 the fp16 search's global key buffers (max_q queries), for K > 64
 // the score rows of one query batch (≤ 1 GiB).

@@ -293,7 +293,8 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const float* __restrict_
   __syncthreads();
   if (threadIdx.x == 0 && ties != nullptr && sm.tflag != 0) {
     const int pos = atomicAdd(ties, 1);
-    ties[1 + pos] = 2 * active[qi] + ((sm.tflag >> 1) & 1);
+    ties[1 + (int64_t)kTieRec * pos] = 2 * active[qi] + ((sm.tflag >> 1) & 1);
+    ties[2 + (int64_t)kTieRec * pos] = -1;  // tie group not collected (K > 64 rows are all resolved on the host)
   }
   for (int e = threadIdx.x; e < K; e += kSelThreads) out[e] = e < n ? (int32_t)(~(uint32_t)(sm.list[e] & 0xffffffffu)) : -1;
 }

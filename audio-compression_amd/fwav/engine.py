@@ -123,6 +123,7 @@ class DeviceCompressed:
     err: Optional[torch.Tensor] = None
     n_active: Optional[torch.Tensor] = None
     energy_partial: Optional[torch.Tensor] = None
+    ties: Optional[torch.Tensor] = None  # fwav_sim_topk's tie list (keep_intermediates)
     n_ties: int = 0          # queries whose top K + 1 scores hold exact ties
     n_resolved: int = 0      # of those, rows re-ranked with numpy's own tie order (fwav.ties)
     empty: bool = False
@@ -171,8 +172,10 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     starts the pool's device→host copy there, on a side stream, so that it overlaps the search).
     ``blas_threads``: the OpenBLAS thread count whose sgemv order the scores follow (default: this process's,
     fwav.ties.blas_threads).  ``tie_order="numpy"`` re-ranks the rows whose match depends on the order of exactly
-    equal scores with numpy's own calls, as the reference does (one host synchronisation to read the count);
-    ``"index"`` keeps the device's (score desc, index asc) order for them (no synchronisation).
+    equal scores with numpy's own calls, as the reference does (one host synchronisation to read the count), so every
+    match tuple is the reference's; ``"numpy_sets"`` also re-ranks every row with a tie at the K-th place, so that
+    the candidate sets are the reference's too; ``"index"`` keeps the device's (score desc, index asc) order (no
+    synchronisation).
     """
     if sig.dim() != 1 or sig.dtype != torch.float32 or not sig.is_cuda:
         raise ValueError("compress_device expects a 1-D float32 device tensor")
@@ -192,8 +195,9 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     lo32 = F32(energy_thresh * 0.5)
     if k > size_call("fwav_topk_max_k"):
         raise ValueError(f"top_k={k} > {size_call('fwav_topk_max_k')} is not supported by the HIP search")
-    if tie_order not in ("numpy", "index"):
-        raise ValueError("tie_order must be 'numpy' (the reference's order of exactly tied scores) or 'index'")
+    if tie_order not in ("numpy", "numpy_sets", "index"):
+        raise ValueError("tie_order must be 'numpy' (the reference's order of exactly tied scores wherever it decides a"
+                         " match), 'numpy_sets' (and wherever it decides a candidate set) or 'index'")
     threads = _ties.blas_threads() if blas_threads is None else int(blas_threads)
     ws_n = size_call("fwav_voiced_workspace_size", n, frame)
     ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
@@ -253,7 +257,8 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
         _mark(events, "sim_topk")
         wk = size_call("fwav_sim_topk_workspace_size", m, nd, k) if (emb16 is not None or k > 64) else 0
         wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
-        ties = torch.empty(m + 1, dtype=torch.int32, device=dev) if tie_order == "numpy" else None
+        ties = (torch.empty(size_call("fwav_tie_list_size", m), dtype=torch.int32, device=dev)
+                if tie_order != "index" else None)
         call("fwav_sim_topk", emb.data_ptr(), _p(emb16), nd, active.data_ptr(), n_active.data_ptr(), m, lo, k, threads,
              cand.data_ptr(), _p(ties), wsk.data_ptr(), wk, st)
         _mark(events, "sim_topk")
@@ -267,7 +272,7 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
             _mark(events, "ties")
             resolve = torch.empty(m + 1, dtype=torch.int32, device=dev)
             call("fwav_tie_check", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, emb.data_ptr(), lo,
-                 threads, ties.data_ptr(), m, resolve.data_ptr(), st)
+                 threads, ties.data_ptr(), m, int(tie_order == "numpy_sets"), resolve.data_ptr(), st)
             counts = torch.stack([ties[0], resolve[0]]).cpu()
             res.n_ties, res.n_resolved = int(counts[0]), int(counts[1])
             if res.n_resolved:
@@ -278,6 +283,8 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     res.pool, res.idx, res.s, res.o, res.sym, res.err, res.n_active = pool, idx, s, o, sym, err, n_active
     if keep_intermediates:
         res.ranges, res.emb, res.cand, res.active = ranges, emb, cand, active
+        if m > 0 and ties is not None:
+            res.ties = ties
     return res
 
 

@@ -15,6 +15,7 @@ from __future__ import annotations
 import hashlib
 import struct
 import wave
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -83,15 +84,37 @@ def _match_records(matches) -> np.ndarray:
     return rec
 
 
+class _Hasher:
+    """SHA-256 of a byte stream on a worker thread (hashlib releases the GIL on large updates), so that hashing
+    overlaps the file reads or writes of the same chunks."""
+
+    def __init__(self):
+        self.sha = hashlib.sha256()
+        self.pool = ThreadPoolExecutor(1)
+        self.pending = None
+
+    def update(self, buf):
+        if self.pending is not None:
+            self.pending.result()
+        self.pending = self.pool.submit(self.sha.update, buf)
+
+    def digest(self) -> bytes:
+        if self.pending is not None:
+            self.pending.result()
+        self.pool.shutdown()
+        return self.sha.digest()
+
+
 def save_compressed(filepath, matches, domains_array, range_size, framerate, sampwidth, tile_size, domain_step,
                     energy_threshold, original_len):
-    """fractal.py:1278-1322 — same bytes, bulk writes."""
+    """fractal.py:1278-1322 — same bytes: the domain rows and the packed match records written as two bulk
+    buffers in chunks, each chunk hashed on a worker thread while the next one is written."""
     rec = _match_records(matches)
     dom = np.ascontiguousarray(np.asarray(domains_array), dtype="<f4")
     n_domains = len(dom)
     hdr = struct.pack(HEADER_FMT, b"FWAV", FWAV_VERSION, range_size, framerate, sampwidth, tile_size, domain_step,
                       energy_threshold, len(rec), n_domains, original_len)
-    sha = hashlib.sha256()
+    sha = _Hasher()
     dbytes = memoryview(dom.reshape(-1).view(np.uint8))
     mbytes = memoryview(rec.view(np.uint8))
     with open(filepath, "wb") as f:
@@ -100,16 +123,32 @@ def save_compressed(filepath, matches, domains_array, range_size, framerate, sam
         for buf in (dbytes, mbytes):
             for i in range(0, len(buf), _CHUNK):
                 piece = buf[i:i + _CHUNK]
-                f.write(piece)
                 sha.update(piece)
+                f.write(piece)
         f.seek(HEADER_SIZE)
         f.write(sha.digest())
+
+
+def _read_into(f, arr: np.ndarray, sha: "_Hasher | None") -> int:
+    """Fill arr's bytes from f in chunks (no intermediate bytes objects); returns the bytes read."""
+    buf = memoryview(arr.reshape(-1).view(np.uint8))
+    got = 0
+    while got < len(buf):
+        n = f.readinto(buf[got:got + _CHUNK])
+        if not n:
+            break
+        if sha is not None:
+            sha.update(buf[got:got + n])
+        got += n
+    return got
 
 
 def load_compressed(filepath, verify_checksum=True):
     """fractal.py:1325-1375 — returns (matches, domains, n_ranges, range_size, framerate, sampwidth, tile_size,
     domain_step, energy_threshold, original_len); ``matches`` is a :class:`MatchList` (a sequence of the
-    reference's ``(int, float, float, int, float)`` tuples backed by arrays)."""
+    reference's ``(int, float, float, int, float)`` tuples backed by arrays).  Both sections are read straight into
+    their final arrays (the domain rows, the packed records whose fields the MatchList views), hashed on a worker
+    thread as they arrive."""
     with open(filepath, "rb") as f:
         if f.read(4) != b"FWAV":
             raise ValueError("Not a FWAV file")
@@ -120,21 +159,17 @@ def load_compressed(filepath, verify_checksum=True):
         (_, _, range_size, framerate, sampwidth, tile_size, domain_step, energy_threshold, n_ranges, n_domains,
          original_len) = struct.unpack(HEADER_FMT, f.read(HEADER_SIZE))
         stored = f.read(32)
-        dom_bytes = f.read(4 * range_size * n_domains)
-        m_bytes = f.read(17 * n_ranges)
-    if verify_checksum:
-        sha = hashlib.sha256()
-        sha.update(dom_bytes)
-        sha.update(m_bytes)
-        if sha.digest() != stored:
-            raise ValueError("Checksum mismatch — file may be corrupted")
+        sha = _Hasher() if verify_checksum else None
+        domains = np.empty((n_domains, range_size), np.float32)
+        rec = np.empty(n_ranges, MATCH_DTYPE)
+        got_d = _read_into(f, domains, sha)
+        got_m = _read_into(f, rec, sha)
+    if sha is not None and sha.digest() != stored:
+        raise ValueError("Checksum mismatch — file may be corrupted")
     if n_domains == 0:
         raise ValueError("need at least one array to concatenate")  # np.vstack([]) in the reference (:1372)
-    if len(dom_bytes) != 4 * range_size * n_domains or len(m_bytes) != 17 * n_ranges:
+    if got_d != domains.nbytes or got_m != rec.nbytes:
         raise ValueError("truncated FWAV file")
-    domains = np.frombuffer(dom_bytes, dtype="<f4").astype(np.float32).reshape(n_domains, range_size)
-    rec = np.frombuffer(m_bytes, dtype=MATCH_DTYPE)
-    matches = MatchList(rec["idx"].astype(np.int32), rec["s"].astype(np.float32), rec["o"].astype(np.float32),
-                        rec["sym"].astype(np.uint8), rec["err"].astype(np.float32))
+    matches = MatchList(rec["idx"], rec["s"], rec["o"], rec["sym"], rec["err"])
     return (matches, domains, n_ranges, range_size, framerate, sampwidth, tile_size, domain_step, energy_threshold,
             original_len)

@@ -97,15 +97,19 @@ int fwav_prune(const float* ranges, int64_t n, int64_t q_offset, int range_size,
  * values — a listed i only needs its cand row), the K domains with the largest f32 score emb[d]·emb[q_offset+i]
  * evaluated in the reference's own BLAS order (OpenBLAS sgemv_t over `blas_threads` threads: the thread split
  * decides which columns its tail kernels score; fwav_common.h), in (score desc, index asc) order, −1-padded when
- * n_domains < K, into cand[i·K .. i·K+K).  ties (device int32[1 + max_q], may be NULL): ties[0] = the number of
- * queries whose top K + 1 scores hold exactly equal values, ties[1 + j] = 2·i + (1 if the K-th and (K+1)-th are
- * equal) — rows whose order (or set) the reference leaves to numpy's argpartition/argsort; see fwav_tie_check.  K ≤ 64: emb16 != NULL selects the fp16 MFMA pre-filter + exact f32 rescoring
+ * n_domains < K, into cand[i·K .. i·K+K).  ties (device int32[fwav_tie_list_size(max_q)], may be NULL): ties[0] =
+ * the number of queries whose top K + 1 scores hold exactly equal values; record j = ties[1 + 9·j .. 10 + 9·j):
+ * [0] = 2·i + (1 if the K-th and (K+1)-th are equal), and for such a K-th place tie [1] = the number of domains
+ * outside the K with the K-th's score (−1: not collected, at most 7), [2 ..] = those domains — the rows whose order
+ * (or set) the reference leaves to numpy's argpartition/argsort; see fwav_tie_check.
+ * K ≤ 64: emb16 != NULL selects the fp16 MFMA pre-filter + exact f32 rescoring
  * kernel, emb16 == NULL the all-f32 MFMA kernel; both return identical candidates.  K > 64 (the module-global
  * top_k is unrestricted in the reference; K ≥ n_domains returns every domain sorted): batched exact score
  * rows + per-query select and sort (fwav_topk_large.hip).  `workspace` holds
  * fwav_sim_topk_workspace_size(max_q, n_domains, k) bytes (unused for K ≤ 64 with emb16 == NULL).
  * 1 ≤ K ≤ fwav_topk_max_k(). */
 int fwav_topk_max_k(void);
+int64_t fwav_tie_list_size(int64_t max_q);
 size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k);
 int fwav_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
                   const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int blas_threads, int32_t* cand,
@@ -147,13 +151,15 @@ int fwav_affine(const float* ranges, int64_t n_ranges, int range_size, const int
                 int64_t n_domains, float s_clip, int32_t* out_idx, float* out_s, float* out_o, uint8_t* out_sym,
                 float* out_err, void* stream);
 /* Tie check (after fwav_affine on the same rows): for every query listed in ties (fwav_sim_topk), decide whether the
- * reference's numpy tie order could change its match — a tie at the K-th place always can; equal scores inside the
- * top K only when two candidates of one run of equal scores both attain the minimum error (fractal.py:816-824).
+ * reference's numpy tie order could change its match (fractal.py:816-824) — equal scores inside the top K when two
+ * candidates of one run of equal scores both attain the minimum error; a tie at the K-th place when some member of
+ * the K-th score's group (in the K or left out) fits no worse than the best candidate outside it, or when the group
+ * was not collected; with exact_sets != 0 every K-th place tie (the candidate sets are then the reference's too).
  * resolve (device int32[1 + max_ties]): resolve[0] = count, resolve[1 + j] = local row to resolve on the host
  * (fwav.ties.resolve_rows: exact score rows, numpy's argpartition/argsort, fwav_affine on those rows). */
 int fwav_tie_check(const float* ranges, int64_t n_ranges, int range_size, const int32_t* cand, int k,
                    const float* pool, int64_t n_domains, const float* emb, int64_t q_offset, int blas_threads,
-                   const int32_t* ties, int64_t max_ties, int32_t* resolve, void* stream);
+                   const int32_t* ties, int64_t max_ties, int exact_sets, int32_t* resolve, void* stream);
 /* Diagnostic (bench roofline, not the product path): n uniformly random rows of rs floats (rs 4/8/16, 16-B aligned
  * table of n_rows rows) gathered with nothing computed — the ceiling of fwav_affine's memory side on this device.
  * sink: one float of device memory. */

@@ -61,7 +61,7 @@ def test_error_codes_without_gpu(lib):
     # K > 64 needs the score-row workspace
     rc = L.fwav_sim_topk(big, None, 10, big, big, 10, 0, 100, 1, big, None, None, 0, None)
     assert rc == -5 and b"workspace" in L.fwav_last_error()
-    rc = L.fwav_tie_check(None, 10, 8, None, 64, None, 100, None, 0, 1, None, 10, None, None)
+    rc = L.fwav_tie_check(None, 10, 8, None, 64, None, 100, None, 0, 1, None, 10, 0, None, None)
     assert rc == -1
     rc = L.fwav_score_rows(None, 100, None, 1, 0, 1, None, None)
     assert rc == -1

@@ -149,6 +149,17 @@ def test_cfg3_numpy_tie_order(cfg3_both):
         out = O.affine(ranges[r:r + 1], ref[None, :], pool)
         for t, v in zip((prod.idx, prod.s, prod.o, prod.sym, prod.err), out):
             assert np.array_equal(t[r:r + 1].cpu().numpy().view(np.uint8), np.asarray(v).view(np.uint8))
+    # K-th place ties the tie check left in index order (every member of the tied group fits worse than the best
+    # candidate outside it): numpy's own ranking gives the same match tuple
+    rec = prod.ties[1:1 + 9 * prod.n_ties].view(-1, 9).cpu().numpy()
+    kept = [int(e >> 1) for e in rec[:, 0] if (e & 1) and int(e >> 1) not in set(diff.tolist())]
+    print(f"cfg3: {int((rec[:, 0] & 1).sum())} K-th place ties, {len(kept)} left in index order")
+    assert len(kept) > 0
+    for r in kept[:8]:
+        ref = O.numpy_topk_row(O.sgemv_scores(emb, emb[r][None, :], kinds)[0], K)
+        out = O.affine(ranges[r:r + 1], ref[None, :], pool)
+        for t, v in zip((prod.idx, prod.s, prod.o, prod.sym, prod.err), out):
+            assert np.array_equal(t[r:r + 1].cpu().numpy().view(np.uint8), np.asarray(v).view(np.uint8)), r
 
 
 def test_cfg3_affine_sampled(cfg3):

@@ -25,9 +25,10 @@ def td(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev())
 
 
-def run_case(g, K):
+def run_case(g, K, tie_order="numpy"):
     p = g["p"]
-    res = engine.compress_device(td(g["signal"]), p["tile"], K, energy_thresh=p["thr"], keep_intermediates=True)
+    res = engine.compress_device(td(g["signal"]), p["tile"], K, energy_thresh=p["thr"], keep_intermediates=True,
+                                 tie_order=tie_order)
     torch.cuda.synchronize()
     return res
 
@@ -46,14 +47,19 @@ def test_ranges_pool_embed(case):
 
 @pytest.mark.parametrize("case", CASES)
 def test_candidates_and_matches(case):
-    """The reference's candidate set for every range and its order wherever the top-K scores are distinct (among
-    exactly equal scores the device keeps index order unless numpy's order can change the match — fwav.ties), and
-    every match tuple bit-exact (SURVEY Appendix A rules 3-4 at their strictest: no exceptions)."""
+    """With tie_order="numpy_sets": the reference's candidate set for every range and its order wherever the top-K
+    scores are distinct (among exactly equal scores the device keeps index order unless numpy's order can change the
+    match — fwav.ties), and every match tuple bit-exact (SURVEY Appendix A rules 3-4 at their strictest: no
+    exceptions).  The product default (tie_order="numpy", K-th place ties re-ranked only where they can decide the
+    match) gives the same tuples."""
     from oracle import fractal_oracle as O
     g = load(case)
     p = g["p"]
     for K in p["Ks"]:  # includes ragged K=2000 >= n_domains (full sort, −1 padded)
-        r = run_case(g, K)
+        d = run_case(g, K)
+        for nm, t in (("idx", d.idx), ("s", d.s), ("o", d.o), ("sym", d.sym), ("err", d.err)):
+            assert bit_equal(t.cpu().numpy(), g[f"m_{nm}_{K}"]), f"{case} K={K} {nm} (default tie order)"
+        r = run_case(g, K, "numpy_sets")
         cand = r.cand.cpu().numpy().reshape(-1, K)
         gold = g[f"cand_{K}"]
         assert all(set(a.tolist()) == set(b.tolist()) for a, b in zip(cand, gold)), f"{case} K={K}: candidate sets"
@@ -68,7 +74,8 @@ def test_candidates_and_matches(case):
                 assert np.array_equal(cand[i], gold[i]), f"{case} K={K} row {i}"
         for nm, t in (("idx", r.idx), ("s", r.s), ("o", r.o), ("sym", r.sym), ("err", r.err)):
             assert bit_equal(t.cpu().numpy(), g[f"m_{nm}_{K}"]), f"{case} K={K} {nm}"
-        print(f"{case} K={K}: {r.n_ties} rows with exact ties, {r.n_resolved} re-ranked by numpy; all tuples exact")
+        print(f"{case} K={K}: {r.n_ties} rows with exact ties, {r.n_resolved} re-ranked by numpy for the sets, "
+              f"{d.n_resolved} for the matches; all tuples exact")
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -140,7 +147,7 @@ def test_reference_e2e_tone(tmp_path):
     assert np.array_equal(np.frombuffer(fw.read_bytes(), np.uint8), g["fwav_32"])
 
 
-def _cands(sig, tile, K, search, thr=1e-4, tie_order="numpy"):
+def _cands(sig, tile, K, search, thr=1e-4, tie_order="numpy_sets"):
     r = engine.compress_device(td(sig), tile, K, energy_thresh=thr, keep_intermediates=True, search=search,
                                tie_order=tie_order)
     torch.cuda.synchronize()

@@ -19,6 +19,10 @@ libs = []
 for path in sys.argv[1:]:
     L = C.CDLL(os.path.abspath(path))
     res, args = SIGNATURES["fwav_sim_topk"]
+    # builds before round 3 have no blas_threads / ties arguments (and no fwav_tie_check)
+    L.new_abi = hasattr(L, "fwav_tie_check")
+    if not L.new_abi:
+        args = args[:8] + args[9:10] + args[11:]
     L.fwav_sim_topk.restype, L.fwav_sim_topk.argtypes = res, args
     libs.append((os.path.basename(path), L))
 cfg = os.environ.get("AB_CFG", "cfg2")  # cfg3: the speech-like 10 min case (its pruned active list)
@@ -63,8 +67,10 @@ for rnd in range(int(os.environ.get("AB_ROUNDS", 4))):
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
+        extra = (int(os.environ.get("AB_THREADS", 16)),) if L.new_abi else ()
+        tie_arg = (None,) if L.new_abi else ()
         rc = L.fwav_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0, 64,
-                             cand.data_ptr(), wsk.data_ptr(), wsn, st)
+                             *extra, cand.data_ptr(), *tie_arg, wsk.data_ptr(), wsn, st)
         e1.record()
         torch.cuda.synchronize()
         assert rc == 0, name
