@@ -1875,9 +1875,13 @@ int fwav_score_rows(const float* emb, int64_t nd, const int32_t* rows, int64_t n
 
 // Diagnostic ablations of the fp16 search kernel (timing only; see k_sim_topk_f16 `dbg`).
 int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t nd, const int32_t* active, const int32_t* n_active,
-                        int64_t max_q, int64_t q_offset, int K, int32_t* cand, void* workspace, int dbg,
+                        int64_t max_q, int64_t q_offset, int K, int32_t* cand, void* workspace, size_t ws_bytes, int dbg,
                         unsigned long long* stats, void* stream) {
   FWAV_CHECK_ARG(emb && emb16 && workspace && K >= 1 && K <= 64, FWAV_ERR_ARG, "fwav_debug_sim_topk: bad args");
+  // the key buffers depend on the work plan of THIS max_q (a split plan for fewer queries can need more than a
+  // whole-block plan for more): a workspace sized for another query count once ran off its end
+  FWAV_CHECK_ARG(ws_bytes >= fwav_sim_topk_workspace_size(max_q, nd, K), FWAV_ERR_WORKSPACE,
+                 "fwav_debug_sim_topk: workspace too small for max_q=%lld", (long long)max_q);
   return launch_topk<128>(emb, (const _Float16*)emb16, nd, active, n_active, max_q, q_offset, K, cand,
                           (hipStream_t)stream, (uint64_t*)workspace, make_sgemv_split(nd, 1), nullptr, dbg, stats);
 }

@@ -42,7 +42,7 @@ SIGNATURES = {
     "fwav_sim_topk_workspace_size": (SZ, [I64, I64, I32]),
     "fwav_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, I32, P, P, P, SZ, P]),
     "fwav_score_rows": (I32, [P, I64, P, I64, I64, I32, P, P]),
-    "fwav_debug_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, I32, P, P]),
+    "fwav_debug_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, SZ, I32, P, P]),
     "fwav_debug_topk_plan": (I32, [I32, I32]),
     "fwav_debug_topk_plan_cover": (I32, [I64, I32, I32, I32, P, P]),
     "fwav_debug_topk_mode": (I32, [I32]),

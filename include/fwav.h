@@ -124,7 +124,7 @@ int fwav_score_rows(const float* emb, int64_t n_domains, const int32_t* rows, in
  * relaunch for overflowed queries only (outputs valid).  Not used by the product path. */
 int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
                         const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand,
-                        void* workspace, int dbg, unsigned long long* stats, void* stream);
+                        void* workspace, size_t ws_bytes, int dbg, unsigned long long* stats, void* stream);
 /* Diagnostic override of the fp16 search's work plan: the last `rt` query blocks are split into `pieces` table
  * ranges, or with pieces == -1 into two query halves (rt < 0 restores the default policy).  Every plan returns the
  * same candidates.  Re-query fwav_sim_topk_workspace_size afterwards. */

@@ -67,6 +67,19 @@ def test_error_codes_without_gpu(lib):
     assert rc == -1
 
 
+def test_debug_search_rejects_workspace_of_another_query_count(lib):
+    """Round 2's memory fault (tools/phase_ab.py): a workspace sized for 41,344 queries was handed to a search of
+    20,672, whose table-pieces plan needs more key buffers.  The debug entry point now takes the workspace size and
+    rejects a short one before any launch; the product always sizes for the query count it launches."""
+    L = lib.lib()
+    nd = 1_321_977
+    small, big_q = L.fwav_sim_topk_workspace_size(41344, nd, 64), L.fwav_sim_topk_workspace_size(20672, nd, 64)
+    assert big_q > small
+    p = ctypes.c_void_p(16)
+    rc = L.fwav_debug_sim_topk(p, p, nd, p, p, 20672, 0, 64, p, p, small, 0, None, None)
+    assert rc == -5 and b"workspace" in L.fwav_last_error()
+
+
 def test_library_digest_matches_sources(lib):
     """The library reports the digest of the sources and flags it was built from, and it is this tree's
     (fwav._lib refuses to bind a library built from anything else)."""

@@ -358,3 +358,43 @@ def test_smoothing_equals_numpy_convolve(w):
         out = torch.empty(nf, dtype=torch.float32, device=dev())
         call("fwav_debug_smooth", et.data_ptr(), nf, w, out.data_ptr(), st)
         assert bit_equal(out.cpu().numpy(), ref), (w, nf)
+
+
+def test_half_of_41344_queries_pieces_plan_stays_in_workspace():
+    """Regression for round 2's memory fault (tools/phase_ab.py): 20,672 queries against the full cfg2 table run the
+    table-pieces plan (every block split, shared limits, k_merge_pieces).  With the workspace sized exactly for that
+    query count, nothing is written past it (1 MiB guard), every emitted index is a domain, and the rows equal the
+    all-f32 kernel's."""
+    from fwav import synth
+    from fwav import engine as E
+    from fwav._lib import size_call
+    sig = td(synth.noise(60.0, 44100, seed=0))
+    tile, K = 2048, 64
+    rs, step = E.geometry(tile)
+    nd = (sig.numel() - tile) // step + 1
+    st = torch.cuda.current_stream().cuda_stream
+    tab = E.embed_tables(rs, sig.device)
+    pool = torch.empty(nd * rs, device=sig.device)
+    emb = torch.empty(nd * 16, device=sig.device)
+    emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device=sig.device)
+    ws = torch.empty(max(size_call("fwav_pool_workspace_size", sig.numel(), tile, rs, step), 16), dtype=torch.uint8,
+                     device=sig.device)
+    call("fwav_pool_embed", sig.data_ptr(), sig.numel(), tile, rs, step, tab.data_ptr(), pool.data_ptr(),
+         emb.data_ptr(), emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+    rows = torch.arange(0, 41344, 2, dtype=torch.int32, device=sig.device)  # the even half, as phase_ab's A
+    max_q = rows.numel()
+    n_act = torch.tensor([max_q], dtype=torch.int32, device=sig.device)
+    out = []
+    for e16 in (emb16.data_ptr(), None):
+        wsn = size_call("fwav_sim_topk_workspace_size", max_q, nd, K)
+        guard = 1 << 20
+        wsk = torch.zeros(wsn + guard, dtype=torch.uint8, device=sig.device)
+        cand = torch.full((41344 * K,), -7, dtype=torch.int32, device=sig.device)
+        call("fwav_sim_topk", emb.data_ptr(), e16, nd, rows.data_ptr(), n_act.data_ptr(), max_q, 0, K, 1,
+             cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
+        torch.cuda.synchronize()
+        assert int(wsk[wsn:].count_nonzero().item()) == 0, "write past the workspace"
+        c = cand.view(-1, K)[rows.long()].cpu().numpy()
+        assert ((c >= 0) & (c < nd)).all()
+        out.append(c)
+    assert np.array_equal(out[0], out[1])

@@ -46,7 +46,7 @@ for path in sys.argv[1:]:
     cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
     stats = torch.zeros(16, dtype=torch.int64, device="cuda")
     rc = L.fwav_debug_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
-                               64, cand.data_ptr(), wsk.data_ptr(), 0, stats.data_ptr(), st)
+                               64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 0, stats.data_ptr(), st)
     torch.cuda.synchronize()
     assert rc == 0
     sv = stats.cpu().tolist()

@@ -38,8 +38,8 @@ for nq in [int(x) for x in os.environ.get("AB_NQ", "41344").split(",")]:
     out = []
     for e16 in (emb16.data_ptr(), None):
         cand = torch.full((nq * 64,), -7, dtype=torch.int32, device="cuda")
-        rc = L.fwav_sim_topk(emb.data_ptr(), e16, nd, active.data_ptr(), n_active.data_ptr(), nq, 0, 64,
-                             cand.data_ptr(), wsk.data_ptr(), wsn, st)
+        rc = L.fwav_sim_topk(emb.data_ptr(), e16, nd, active.data_ptr(), n_active.data_ptr(), nq, 0, 64, 16,
+                             cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
         torch.cuda.synchronize()
         assert rc == 0
         out.append(cand.view(nq, 64))

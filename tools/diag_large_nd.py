@@ -46,7 +46,7 @@ cand16 = res.cand.view(m, K).cpu().numpy()
 act = torch.arange(m, dtype=torch.int32, device="cuda")
 na = torch.tensor([m], dtype=torch.int32, device="cuda")
 c32 = torch.full((m * K,), -7, dtype=torch.int32, device="cuda")
-call("fwav_sim_topk", emb.data_ptr(), None, nd, act.data_ptr(), na.data_ptr(), m, lo, K, c32.data_ptr(), None, 0,
+call("fwav_sim_topk", emb.data_ptr(), None, nd, act.data_ptr(), na.data_ptr(), m, lo, K, 16, c32.data_ptr(), None, None, 0,
      torch.cuda.current_stream().cuda_stream)
 torch.cuda.synchronize()
 c32 = c32.view(m, K).cpu().numpy()

@@ -51,10 +51,10 @@ for plan in [(0, 1), (-1, 1)]:
         cand = torch.full((nr * K,), -7, dtype=torch.int32, device="cuda")
         if dbg < 0:  # production kernel
             call("fwav_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
-                 K, cand.data_ptr(), wsk.data_ptr(), wsn, st)
+                 K, 16, cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
         else:
             call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(),
-                 nr, 0, K, cand.data_ptr(), wsk.data_ptr(), dbg | 16384, None, st)
+                 nr, 0, K, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), dbg | 16384, None, st)
         torch.cuda.synchronize()
         c = cand.cpu().numpy().reshape(-1, K)
         bad = np.nonzero(~np.all(c == ref, axis=1))[0]
@@ -74,7 +74,7 @@ wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
 stats = torch.zeros(16 + nr + 512, dtype=torch.int64, device="cuda")
 cand = torch.full((nr * K,), -7, dtype=torch.int32, device="cuda")
 call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0, K,
-     cand.data_ptr(), wsk.data_ptr(), 32768, stats.data_ptr(), st)
+     cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 32768, stats.data_ptr(), st)
 torch.cuda.synchronize()
 seeds = stats[16:16 + nr].cpu().numpy().astype(np.uint32).view(np.float32)
 E16 = emb16.cpu().numpy().reshape(-1, 2, 256, 8).transpose(0, 2, 1, 3).reshape(-1, 16)[:nd].astype(np.float64)

@@ -45,8 +45,8 @@ L.fwav_debug_topk_plan(0, 1)
 wsn = L.fwav_sim_topk_workspace_size(nr, nd, K)
 wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
 cand = torch.full((nr * K,), -7, dtype=torch.int32, device="cuda")
-assert L.fwav_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0, K,
-                       cand.data_ptr(), wsk.data_ptr(), wsn, st) == 0
+assert L.fwav_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0, K, 16,
+                       cand.data_ptr(), None, wsk.data_ptr(), wsn, st) == 0
 torch.cuda.synchronize()
 c = cand.cpu().numpy().reshape(-1, K)
 print("rows differing from f32:", np.nonzero(~np.all(c == ref, axis=1))[0][:20])

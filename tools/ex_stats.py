@@ -40,7 +40,7 @@ stats = torch.zeros(16, dtype=torch.int64, device="cuda")
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
 call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0, 64,
-     cand.data_ptr(), wsk.data_ptr(), 1 << 17, stats.data_ptr(), st)
+     cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 1 << 17, stats.data_ptr(), st)
 e1.record()
 torch.cuda.synchronize()
 o = wsn - 4 - 4 * max(nq, 1)  # workspace tail: ovf list, its count, then u32 seeds[q]

@@ -44,7 +44,7 @@ for rep in range(2):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
-         64, cand.data_ptr(), wsk.data_ptr(), 0, stats.data_ptr(), st)
+         64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 0, stats.data_ptr(), st)
     e1.record()
     torch.cuda.synchronize()
     sv = stats.cpu().tolist()

@@ -42,7 +42,7 @@ for nq in [int(x) for x in os.environ.get("AB_NQ", "131072,262144,330750").split
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rc = L.fwav_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0, 64,
-                             cand.data_ptr(), wsk.data_ptr(), wsn, st)
+                             16, cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
         e1.record()
         torch.cuda.synchronize()
         assert rc == 0

@@ -4,8 +4,10 @@ around q − left) of its left neighbour's top K and the mirrored shifts of its 
 of those distinct domains (exact f32, minus 2δ) is a valid band limit.  Times A and B with an -DFWAV_TOPK_EXTSEED
 build (the seeds come from torch here; a device kernel would compute them) and checks that A ∪ B equals the
 one-phase result.  usage: [AB_NQ=...] python tools/phase_ab.py tools/ab/libfwav_ext.so [shifts]
-Caution: the AB_NQ=41344 run (table pieces + external seeds, a combination the product never launches) ended in a
-memory fault inside a later torch gather; the cause was not found, so do not rerun that case unchanged."""
+The AB_NQ=41344 run of round 2 ended in a memory fault: this script sized the key workspace for nq queries but
+searched nq/2 (a table-pieces plan, which needs more: 258.4 vs 255.6 MB at cfg2), so the kernel wrote past the end
+of its workspace.  fwav_debug_sim_topk now takes the workspace size and rejects a short one; the workspace here is
+sized for every query count it searches."""
 import ctypes as C
 import os
 import sys
@@ -46,7 +48,8 @@ call("fwav_pool_embed", sig.data_ptr(), sig.numel(), tile, rs, step, tab.data_pt
 # cfg2: every range; cfg3: the first n_active ranges (as tools/ab_topk.py)
 nq = int(os.environ.get("AB_NQ", nr if cfg == "cfg2" else int(r.n_active.item())))
 act_all = torch.arange(nq, dtype=torch.int32, device="cuda")
-wsn = L.fwav_sim_topk_workspace_size(nq, nd, 64)
+# the plan (and so the key workspace) depends on the query count: size for every count searched below
+wsn = max(L.fwav_sim_topk_workspace_size(n, nd, 64) for n in (nq, nq // 2, nq - nq // 2))
 wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
 E = emb.view(nd, 16)
 d16 = 2.0e-3
@@ -60,7 +63,7 @@ def search(active, seeds=None, reps=4):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rc = L.fwav_debug_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(),
-                                   active.numel(), 0, 64, cand.data_ptr(), wsk.data_ptr(), 0,
+                                   active.numel(), 0, 64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 0,
                                    seeds.data_ptr() if seeds is not None else None, st)
         e1.record()
         torch.cuda.synchronize()

@@ -52,7 +52,7 @@ for rnd in range(3):
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
             call("fwav_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
-                 64, cand.data_ptr(), wsk.data_ptr(), wsn, st)
+                 64, 16, cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))

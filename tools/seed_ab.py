@@ -57,7 +57,7 @@ for S in [0] + [int(x) for x in sys.argv[2:]]:
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         rc = L.fwav_debug_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
-                                   64, cand.data_ptr(), wsk.data_ptr(), 0, seeds.data_ptr(), st)
+                                   64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 0, seeds.data_ptr(), st)
         e1.record()
         torch.cuda.synchronize()
         assert rc == 0

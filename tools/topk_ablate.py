@@ -34,7 +34,7 @@ from fwav._lib import size_call
 wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nr, nd, 64), dtype=torch.uint8, device="cuda")
 stats = torch.zeros(16, dtype=torch.int64, device="cuda")  # kStats = 12 used
 call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
-     64, cand.data_ptr(), wsk.data_ptr(), 0, stats.data_ptr(), st)
+     64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 0, stats.data_ptr(), st)
 torch.cuda.synchronize()
 sv = stats.cpu().tolist()
 waves = (nr + 255) // 256 * 8
@@ -49,7 +49,7 @@ print("per-wave share of kernel ticks: barrier %.3f, streaming %.3f, replays %.3
 for dbg in (1, 4):
     stats.zero_()
     call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
-         64, cand.data_ptr(), wsk.data_ptr(), dbg, stats.data_ptr(), st)
+         64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), dbg, stats.data_ptr(), st)
     torch.cuda.synchronize()
     sv = stats.cpu().tolist()
     tot = sv[6]
@@ -65,6 +65,6 @@ for dbg in ([int(x) for x in sys.argv[2].split(',')] if len(sys.argv) > 2 else [
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
-             64, cand.data_ptr(), wsk.data_ptr(), dbg, None, st)
+             64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), dbg, None, st)
         e1.record(); torch.cuda.synchronize()
     print(f"dbg={dbg}: {e0.elapsed_time(e1):.2f} ms", flush=True)

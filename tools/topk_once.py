@@ -37,6 +37,6 @@ cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
 wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nr, nd, 64), dtype=torch.uint8, device="cuda")
 for _ in range(2):
     call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
-         64, cand.data_ptr(), wsk.data_ptr(), dbg, None, st)
+         64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), dbg, None, st)
 torch.cuda.synchronize()
 print("done", dbg)

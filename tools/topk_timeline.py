@@ -39,7 +39,7 @@ for _ in range(2):
     stats.zero_()
     stats[16::2] = 2**62
     call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
-         64, cand.data_ptr(), wsk.data_ptr(), 4096 | extra, stats.data_ptr(), st)
+         64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 4096 | extra, stats.data_ptr(), st)
     torch.cuda.synchronize()
 tl = stats[16:].cpu().numpy().reshape(-1, 2)
 tl = tl[tl[:, 0] < 2**62].astype(np.float64)
