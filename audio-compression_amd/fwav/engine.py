@@ -101,7 +101,7 @@ def _zero_cand_device(n_domains: int, top_k: int, device: torch.device) -> torch
 
 @dataclasses.dataclass
 class DeviceCompressed:
-    """Result of :func:`compress_device`.  Device tensors; ``finalize()`` synchronises once."""
+    """Result of :func:`compress_device`.  Device tensors (final once ``wait()`` returns)."""
 
     n_ranges: int
     range_size: int
@@ -127,6 +127,14 @@ class DeviceCompressed:
     n_ties: int = 0          # queries whose top K + 1 scores hold exact ties
     n_resolved: int = 0      # of those, rows re-ranked with numpy's own tie order (fwav.ties)
     empty: bool = False
+    pending: Optional[object] = None  # deferred tie resolution (compress_device(defer_ties=True)): a Future
+
+    def wait(self) -> "DeviceCompressed":
+        """Complete a deferred tie resolution (no-op otherwise); the outputs are final afterwards."""
+        if self.pending is not None:
+            self.pending.result()
+            self.pending = None
+        return self
 
     def is_silent(self) -> bool:
         """np.sum((signal·mask)²) < 1e-8 (fractal.py:1083): the device computes numpy's float32 sum bit-exactly, and the
@@ -160,7 +168,7 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
                      fast_mode: bool = True, s_clip: float = 16.0, shard: Optional[tuple[int, int]] = None,
                      keep_intermediates: bool = False, events: Optional[dict] = None,
                      search: str = "f16", on_pool=None, blas_threads: Optional[int] = None,
-                     tie_order: str = "numpy") -> DeviceCompressed:
+                     tie_order: str = "numpy", defer_ties: bool = False) -> DeviceCompressed:
     """Run the compress hot path on ``sig`` (1-D float32 tensor on a HIP device).
 
     ``shard=(lo, hi)`` restricts candidate search and the affine solve to ranges ``[lo, hi)`` (the
@@ -175,7 +183,9 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     equal scores with numpy's own calls, as the reference does (one host synchronisation to read the count), so every
     match tuple is the reference's; ``"numpy_sets"`` also re-ranks every row with a tie at the K-th place, so that
     the candidate sets are the reference's too; ``"index"`` keeps the device's (score desc, index asc) order (no
-    synchronisation).
+    synchronisation).  ``defer_ties=True`` hands that host step to a background thread (its device work on a side
+    stream, after this call's kernels) and returns at once: the outputs are final after ``result.wait()``, so a
+    stream of calls overlaps one call's host ranking with the next call's search.
     """
     if sig.dim() != 1 or sig.dtype != torch.float32 or not sig.is_cuda:
         raise ValueError("compress_device expects a 1-D float32 device tensor")
@@ -273,12 +283,19 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
             resolve = torch.empty(m + 1, dtype=torch.int32, device=dev)
             call("fwav_tie_check", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, emb.data_ptr(), lo,
                  threads, ties.data_ptr(), m, int(tie_order == "numpy_sets"), resolve.data_ptr(), st)
-            counts = torch.stack([ties[0], resolve[0]]).cpu()
-            res.n_ties, res.n_resolved = int(counts[0]), int(counts[1])
-            if res.n_resolved:
-                _ties.resolve_rows(resolve[1:1 + res.n_resolved], emb=emb, n_domains=nd, q_offset=lo, k=k,
-                                   threads=threads, ranges=rsh, range_size=rs, pool=pool, s_clip=sc, cand=cand,
-                                   outs=(idx, s, o, sym, err), stream=st)
+
+            def finish(stream_id):
+                counts = torch.stack([ties[0], resolve[0]]).cpu()
+                res.n_ties, res.n_resolved = int(counts[0]), int(counts[1])
+                if res.n_resolved:
+                    _ties.resolve_rows(resolve[1:1 + res.n_resolved], emb=emb, n_domains=nd, q_offset=lo, k=k,
+                                       threads=threads, ranges=rsh, range_size=rs, pool=pool, s_clip=sc, cand=cand,
+                                       outs=(idx, s, o, sym, err), stream=stream_id)
+
+            if defer_ties:
+                res.pending = _ties.defer(finish, dev)
+            else:
+                finish(st)
             _mark(events, "ties")
     res.pool, res.idx, res.s, res.o, res.sym, res.err, res.n_active = pool, idx, s, o, sym, err, n_active
     if keep_intermediates:

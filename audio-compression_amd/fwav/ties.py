@@ -67,11 +67,62 @@ def numpy_topk_row(scores: np.ndarray, k: int) -> np.ndarray:
     return out
 
 
+_POOL = None
+_PINNED: dict = {}
+_DRIVER = None
+_SIDE: dict = {}
+
+
+def defer(finish, device: torch.device):
+    """Run ``finish(stream)`` — the host half of a tie resolution — on the background driver thread, on a side stream
+    that first waits for everything queued so far on ``device``'s current stream.  Returns its Future.  One driver
+    thread: resolutions run in call order and share the staging buffers."""
+    global _DRIVER
+    if _DRIVER is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _DRIVER = ThreadPoolExecutor(1, thread_name_prefix="fwav-ties-driver")
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(device))
+    key = str(device)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device)
+    side = _SIDE[key]
+
+    def job():
+        with torch.cuda.device(device), torch.cuda.stream(side):
+            side.wait_event(ev)
+            finish(side.cuda_stream)
+            side.synchronize()
+
+    return _DRIVER.submit(job)
+
+
+def _pool():
+    """Host threads for numpy's ranking of the exact score rows (argpartition runs outside the GIL; the box's 16-CPU
+    share: 8 threads measured 5.7x one at cfg2 row widths, profiles/r03/host_tie_cost.log)."""
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        n = int(os.environ.get("FWAV_TIE_THREADS", "8"))
+        _POOL = ThreadPoolExecutor(max(1, n), thread_name_prefix="fwav-ties")
+    return _POOL
+
+
+def _pinned(slot: int, numel: int) -> torch.Tensor:
+    """A reusable page-locked staging buffer (float32), one per double-buffer slot."""
+    t = _PINNED.get(slot)
+    if t is None or t.numel() < numel:
+        t = torch.empty(numel, dtype=torch.float32, pin_memory=True)
+        _PINNED[slot] = t
+    return t[:numel]
+
+
 def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, k: int, threads: int,
                  ranges: torch.Tensor, range_size: int, pool: torch.Tensor, s_clip: float, cand: torch.Tensor,
                  outs: tuple, stream: int) -> None:
-    """Rows (local indices, device int32) whose match depends on numpy's tie order: exact score rows in batches,
-    numpy's ranking on the host, the new candidate rows written back to ``cand`` and the affine solve re-run for those
+    """Rows (local indices, device int32) whose match depends on numpy's tie order: exact score rows in batches
+    (fwav_score_rows, copied to page-locked memory while the host ranks the previous batch), numpy's ranking of each
+    row on a host thread pool, the new candidate rows written back to ``cand`` and the affine solve re-run for those
     rows into ``outs`` = (idx, s, o, sym, err)."""
     dev = rows.device
     n = rows.numel()
@@ -80,16 +131,28 @@ def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_off
     nd = int(n_domains)
     per = max(1, min(n, ROW_BUDGET // (4 * nd)))
     cv = cand.view(-1, k)
-    new_rows = []
-    for b0 in range(0, n, per):
+    ex = _pool()
+    futs = []
+    S = torch.empty(per * nd, dtype=torch.float32, device=dev)
+    ev = [torch.cuda.Event(), torch.cuda.Event()]
+    staged = []
+    for bi, b0 in enumerate(range(0, n, per)):
         rb = rows[b0:b0 + per].contiguous()
         m = rb.numel()
-        S = torch.empty(m * nd, dtype=torch.float32, device=dev)
+        if bi >= 2:  # the staging slot about to be overwritten: its rows are ranked already
+            for f in staged[bi - 2]:
+                f.result()
         call("fwav_score_rows", emb.data_ptr(), nd, rb.data_ptr(), m, int(q_offset), int(threads), S.data_ptr(),
              stream)
-        Sh = S.view(m, nd).cpu().numpy()
-        new_rows.append(np.stack([numpy_topk_row(Sh[i], k) for i in range(m)]))
-    newc = torch.from_numpy(np.concatenate(new_rows)).to(dev)
+        h = _pinned(bi & 1, m * nd)
+        h.copy_(S[:m * nd], non_blocking=True)
+        ev[bi & 1].record()
+        ev[bi & 1].synchronize()  # S is reused by the next batch and h is read by the threads
+        Sh = h.numpy().reshape(m, nd)
+        batch = [ex.submit(numpy_topk_row, Sh[i], k) for i in range(m)]
+        staged.append(batch)
+        futs.extend(batch)
+    newc = torch.from_numpy(np.stack([f.result() for f in futs])).to(dev)
     ridx = rows.long()
     cv[ridx] = newc
     rs = int(range_size)

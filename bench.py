@@ -128,6 +128,34 @@ def affine_hbm_roofline(dev, K: int, n_queries: int = 262_144, reps: int = 10) -
                         f"{nd} rows ({nd * rs * 4 / 1e9:.2f} GB, above the 256 MB MALL)"}
 
 
+def fwav_io_bench() -> dict:
+    """SURVEY §8(f) rank 1 at the size that motivates it: save_compressed / load_compressed of a cfg4-shaped .fwav
+    (86,398,977 x 8 domain rows + 21,600,000 match records = 3.13 GB).  Values are seeded random (the I/O path does
+    not look at them; byte identity with the reference's format is tests/test_host.py's job)."""
+    import tempfile
+    from fwav import fwavio
+    from fwav.matches import MatchList
+    nd, nr, rs = 86_398_977, 21_600_000, 8
+    rng = np.random.default_rng(0)
+    dom = rng.standard_normal((nd, rs), dtype=np.float32)
+    m = MatchList(rng.integers(0, nd, nr, dtype=np.int32), rng.standard_normal(nr, dtype=np.float32),
+                  rng.standard_normal(nr, dtype=np.float32), rng.integers(0, 2, nr, dtype=np.uint8),
+                  rng.random(nr, dtype=np.float32))
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "cfg4.fwav")
+        t0 = time.perf_counter()
+        fwavio.save_compressed(p, m, dom, rs, 48000, 4, 2048, 2, 1e-4, 172_800_000)
+        t_save = time.perf_counter() - t0
+        size = os.path.getsize(p)
+        t0 = time.perf_counter()
+        out = fwavio.load_compressed(p)
+        t_load = time.perf_counter() - t0
+        ok = bool(np.array_equal(out[1], dom) and np.array_equal(out[0].idx, m.idx) and np.array_equal(out[0].err, m.err))
+    return {"bytes": size, "save_ms": t_save * 1e3, "save_gbs": size / t_save / 1e9, "load_ms": t_load * 1e3,
+            "load_gbs": size / t_load / 1e9, "roundtrip_equal": ok, "checksum": "SHA-256 verified on load",
+            "note": "cfg4 shape, seeded random values; one SHA-256 stream over the body bounds both directions"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -160,7 +188,11 @@ def main():
     phase = {}
     if world == 1:
         def step(ev=None):
-            return engine.compress_device(sig, tile, K, energy_thresh=1e-4, events=ev)
+            # the host half of numpy-order tie resolution (a few rows per step) overlaps the next step's search;
+            # every step's outputs are final (wait()) before the timed region closes
+            r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, events=ev, defer_ties=True)
+            step.pending.append(r)
+            return r
     else:
         def step(ev=None, phases=False):
             def compute(s, t, k, thr, shard):
@@ -178,8 +210,18 @@ def main():
             step.out = out
             return step.last
 
+    if world == 1:
+        step.pending = []
+
+    def drain():
+        for r in getattr(step, "pending", []):
+            r.wait()
+        if world == 1:
+            step.pending = []
+
     for _ in range(args.warmup):
         res = step()
+    drain()
     torch.cuda.synchronize()
     phase.clear()
 
@@ -195,6 +237,7 @@ def main():
         ev = {}
         res = step(ev)
         evs.append(ev)
+    drain()
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -292,6 +335,18 @@ def main():
                        f"{nr * (12 * rs + 17) / 1e6:.1f} MB per iteration")
         dec["streaming_equivalent_gbs_forced50"] = nr * (12 * rs + 17) * 50 / (dec["forced50"]["ms"] * 1e-3) / 1e9
         line["decode"] = dec
+        # numpy-order ties, synchronously (the timed steps defer the host half): how many rows the search lists, how
+        # many the device-side check sends to numpy, and what that costs in one call
+        tev = {}
+        rt = engine.compress_device(sig, tile, K, energy_thresh=1e-4, events=tev)
+        torch.cuda.synchronize()
+        line["ties"] = {"rows_with_exact_ties": rt.n_ties, "rows_ranked_by_numpy": rt.n_resolved,
+                        "ms_synchronous": tev["ties"][0].elapsed_time(tev["ties"][1]),
+                        "note": "timed steps overlap this host work with the next step's search (defer_ties)"}
+        try:
+            line["fwav_io_cfg4"] = fwav_io_bench()
+        except Exception as e:  # noqa: BLE001
+            line["fwav_io_cfg4"] = {"error": str(e)[:200]}
         line["roofline_affine"] = affine_hbm_roofline(dev, K)
         line["roofline_affine_in_pipeline"] = {
             "achieved": nr * (4 * rs + 4 * K + 4 * K * rs + 17) / (stage_ms["affine"] * 1e-3) / 1e9,
