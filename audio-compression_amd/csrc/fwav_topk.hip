@@ -1935,6 +1935,24 @@ int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t*
   return FWAV_OK;
 }
 
+// The first pass fwav_sim_topk would launch for max_q queries over nd domains on the current device (no launch):
+// geometry (1 = wide), first-pass mode (0 = S16, 1 = HL), whole-table blocks F, split blocks R, pieces P (−1: query
+// halves), grid.
+int fwav_debug_topk_plan_info(int64_t max_q, int64_t nd, int32_t* info, int64_t* blocks) {
+  FWAV_CHECK_ARG(max_q >= 0 && nd > 0 && info && blocks, FWAV_ERR_ARG, "fwav_debug_topk_plan_info: bad args");
+  const bool wide = wide_geometry(nd);
+  int rt, P;
+  host_plan_for(max_q, nd, wide, rt, P);
+  const TopkPlan pl = make_plan(max_q, rt, P, wide ? kWideQB : k16QB);
+  info[0] = wide ? 1 : 0;
+  info[1] = first_mode(nd);
+  info[2] = pl.halves ? -1 : pl.P;
+  blocks[0] = pl.F;
+  blocks[1] = pl.R;
+  blocks[2] = pl.items();
+  return FWAV_OK;
+}
+
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.
 int fwav_debug_topk_plan(int rt, int pieces) {

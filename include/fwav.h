@@ -129,6 +129,11 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, 
  * ranges, or with pieces == -1 into two query halves (rt < 0 restores the default policy).  Every plan returns the
  * same candidates.  Re-query fwav_sim_topk_workspace_size afterwards. */
 int fwav_debug_topk_plan(int rt, int pieces);
+/* The first pass fwav_sim_topk would launch for max_q queries over n_domains domains on the current device (host
+ * only): info[0] = geometry (1 = wide), info[1] = first-pass mode (0 = fp16 band, 1 = hi/lo band), info[2] = table
+ * pieces per split block (−1: query halves); blocks[0] = whole-table blocks, blocks[1] = split blocks,
+ * blocks[2] = grid. */
+int fwav_debug_topk_plan_info(int64_t max_q, int64_t n_domains, int32_t* info, int64_t* blocks);
 /* Host-side check of a work plan (no device): count[position] += 1 for every query slot of every item of the plan of
  * n queries (whole blocks and query halves cover a query once, a block in P table pieces P times); *items = grid. */
 int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t* count, int64_t* items);

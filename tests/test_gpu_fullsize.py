@@ -239,3 +239,38 @@ def test_cfg2_whole_search_equals_f32():
     cand = res.cand.view(-1, K).cpu().numpy()
     assert (cand >= 0).all() and (cand < res.n_domains).all()
     assert np.array_equal(cand, f32_search(res, np.arange(res.n_ranges), K))
+
+
+def test_cfg4_shard_wide_geometry_default():
+    """A cfg4 shard of 337,500 consecutive queries (one rank's share of 64) against the whole 86.4 M-domain table —
+    where the wide geometry (16 waves × 32 queries, one workgroup per CU) is the default first pass.  The plan is
+    asserted to be the wide one with whole-table blocks; every row equals the base-geometry search (8 waves, a
+    different plan and processing order), 1,024 rows equal the all-f32 kernel (a VALU scan of the 5.5 GB table per
+    128-query workgroup takes tens of seconds at this size), and sampled rows hold the exact top
+    K (fractal.py:535-541)."""
+    sig, _, _ = synth.make_config_signal("cfg4", seed=0)
+    q = 337_500
+    x = torch.from_numpy(sig).to(dev())
+    res = engine.compress_device(x, 2048, K, shard=(0, q), keep_intermediates=True, tie_order="index")
+    torch.cuda.synchronize()
+    nd = res.n_domains
+    info = np.zeros(3, np.int32)
+    blocks = np.zeros(3, np.int64)
+    call("fwav_debug_topk_plan_info", q, nd, info.ctypes.data, blocks.ctypes.data)
+    print(f"cfg4 shard plan: wide {info[0]} mode {info[1]} pieces {info[2]} whole blocks {blocks[0]} split "
+          f"{blocks[1]} grid {blocks[2]}")
+    assert info[0] == 1 and blocks[0] > 0 and blocks[0] * 512 >= q // 2
+    wide = res.cand.view(-1, K).cpu().numpy()
+    assert (wide >= 0).all() and (wide < nd).all()
+    call("fwav_debug_topk_geometry", 0)
+    try:
+        base = engine.compress_device(x, 2048, K, shard=(0, q), keep_intermediates=True, tie_order="index")
+        torch.cuda.synchronize()
+    finally:
+        call("fwav_debug_topk_geometry", -1)
+    assert np.array_equal(wide, base.cand.view(-1, K).cpu().numpy())
+    rows = np.arange(0, q, q // 1024)[:1024]
+    assert np.array_equal(wide[rows], f32_search(res, rows, K))
+    emb_t = res.emb.view(-1, 16)
+    for j in rows[::128]:
+        check_topk_property(emb_t, int(j), wide[j], K)
