@@ -7,9 +7,11 @@
 //
 // Contract: for every active query q (a range index; its query vector is domain-embedding row q), write
 // the K domains with the largest f32 score s(q,d) = emb[d]·emb[q] evaluated in the reference's own order (numpy →
-// OpenBLAS sgemv, fwav_common.h sgemv16), in (score desc, index asc) order, −1-padded when nd < K.  With the scores
-// bit-identical to the reference's, candidate sets can differ from it only where exactly equal scores straddle the
-// K-th place (numpy's introselect then picks among them; SURVEY Appendix A rule 3).
+// OpenBLAS sgemv_t: its 4-column microkernel, and for the last columns of each BLAS thread's chunk the 4x2 / 4x1
+// tail kernels — fwav_common.h sgemv16 / sgemv_kind, pinned column by column against numpy), in (score desc,
+// index asc) order, −1-padded when nd < K.  The scores being the reference's bit for bit, the result can differ from
+// the reference's only among exactly equal scores, whose order (and, at the K-th place, set) numpy's introselect /
+// argsort decide: every such query is listed in `ties` (record_tie) for fwav_tie_check / fwav.ties.
 //
 // The n_ranges × n_domains score matrix (4.4e11 entries at cfg2) is never materialised.
 //

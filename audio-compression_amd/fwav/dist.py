@@ -36,6 +36,9 @@ FIELDS = ("idx", "s", "o", "sym", "err")
 
 
 # ------------------------------------------------------------------------------------------------ helpers
+#: longest range the range-sharded decode keeps in registers (fwav_decode.hip kMaxResidentRs)
+RESIDENT_MAX_RS = 32
+
 def _coll_device(group, device: torch.device) -> torch.device:
     """Where collective buffers live: the GPU for RCCL, the host for gloo."""
     return device if dist.get_backend(group) == "nccl" else torch.device("cpu")
@@ -333,6 +336,23 @@ def decompress_sharded(matches_soa: Optional[dict], domains: Optional[np.ndarray
         meta[0], meta[1], meta[2] = int(n_ranges), int(np.asarray(domains).shape[0]), int(range_size)
     _broadcast_(meta, group, device)
     nr, nd, rs = (int(v) for v in meta.cpu().tolist())
+    if decoder is None and rs > RESIDENT_MAX_RS:
+        # the sharded kernels keep a range in registers (fwav_decode_run: range_size ≤ 32, tile ≤ 8447); longer
+        # ranges decode on rank 0 alone with the single-device streaming path — every rank learnt rs from the one
+        # broadcast above, so all of them leave here together, before any other collective
+        if rank != 0:
+            return None
+        from . import engine
+        td = lambda a, t: torch.from_numpy(np.ascontiguousarray(a, dtype=t)).to(device)  # noqa: E731
+        rec, ran, deltas = engine.decompress_device(
+            td(matches_soa["idx"], np.int32), td(matches_soa["s"], np.float32), td(matches_soa["o"], np.float32),
+            td(np.asarray(matches_soa["sym"]).astype(np.uint8), np.uint8),
+            td(np.asarray(domains).reshape(-1), np.float32), nr, rs, iterations, convergence_eps, s_clip, s_damping)
+        out = rec.cpu().numpy()
+        if original_len is not None:
+            out = out[:original_len]
+        tm.update(decode_s=time.perf_counter() - t0)
+        return out, dict(iterations=ran, deltas=deltas, blocks=[(0, nr)] + [(nr, nr)] * (world - 1))
     pool = torch.empty(max(nd * rs, 1), dtype=torch.float32, device=device)
     if rank == 0 and nd:
         pool[:nd * rs].copy_(torch.from_numpy(np.ascontiguousarray(domains, dtype=np.float32).reshape(-1)))

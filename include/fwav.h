@@ -125,7 +125,12 @@ int fwav_score_rows(const float* emb, int64_t n_domains, const int32_t* rows, in
 int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
                         const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand,
                         void* workspace, size_t ws_bytes, int dbg, unsigned long long* stats, void* stream);
-/* Diagnostic override of the fp16 search's work plan: the last `rt` query blocks are split into `pieces` table
+/* The three overrides below (fwav_debug_topk_plan / _mode / _geometry) are PROCESS-GLOBAL test knobs, not thread-safe:
+ * they change which kernels fwav_sim_topk launches and how much workspace it needs, so set them only while no search
+ * is being sized or is in flight on any thread, and re-query fwav_sim_topk_workspace_size after a change (a search
+ * sized before the change is rejected with FWAV_ERR_WORKSPACE when it needs more).  The product never sets them.
+ *
+ * Diagnostic override of the fp16 search's work plan: the last `rt` query blocks are split into `pieces` table
  * ranges, or with pieces == -1 into two query halves (rt < 0 restores the default policy).  Every plan returns the
  * same candidates.  Re-query fwav_sim_topk_workspace_size afterwards. */
 int fwav_debug_topk_plan(int rt, int pieces);

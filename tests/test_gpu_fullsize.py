@@ -245,8 +245,7 @@ def test_cfg4_shard_wide_geometry_default():
     """A cfg4 shard of 337,500 consecutive queries (one rank's share of 64) against the whole 86.4 M-domain table —
     where the wide geometry (16 waves × 32 queries, one workgroup per CU) is the default first pass.  The plan is
     asserted to be the wide one with whole-table blocks; every row equals the base-geometry search (8 waves, a
-    different plan and processing order), 1,024 rows equal the all-f32 kernel (a VALU scan of the 5.5 GB table per
-    128-query workgroup takes tens of seconds at this size), and sampled rows hold the exact top
+    different plan and processing order), 1,024 rows equal the all-f32 kernel, and sampled rows hold the exact top
     K (fractal.py:535-541)."""
     sig, _, _ = synth.make_config_signal("cfg4", seed=0)
     q = 337_500
