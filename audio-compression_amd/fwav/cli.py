@@ -4,8 +4,10 @@
   python fractal.py decompress IN [--out PATH] [--iter 8] [--eps 1e-3] [--gpu] [--batch] [--workers 4]
 
 Non-batch OUTPUT / --out are used as directories (quirk Q8, fractal.py:1509, 1538).  Batch mode skips
-files whose output exists and writes compression_metrics.json / decompression_metrics.json.  Worker
-processes are started with 'spawn' (never fork after HIP initialisation); each opens the device itself.
+files whose output exists and writes compression_metrics.json / decompression_metrics.json.  The reference's
+file-level Pool (fractal.py:1596-1600, 1640-1644) becomes one worker process per GPU (at most --workers of them):
+each worker is pinned to its own device at start-up and takes files from the shared queue, so a node's GPUs work
+on different files at once.  Workers are started with 'spawn' (never fork after HIP initialisation).
 """
 from __future__ import annotations
 
@@ -28,12 +30,36 @@ def _decompress_job(args):
     return process_file_decompress(*args)
 
 
+def _pin_device(counter, n_gpus):
+    """Pool initializer: worker k of the pool takes GPU k (one process per GPU)."""
+    with counter.get_lock():
+        k = counter.value
+        counter.value += 1
+    if n_gpus > 0:
+        import torch
+        torch.cuda.set_device(k % n_gpus)
+
+
+def _gpu_count() -> int:
+    """Visible GPUs, counted without initialising HIP in this (parent) process."""
+    try:
+        import torch
+        return int(torch.cuda.device_count())
+    except Exception:  # noqa: BLE001
+        return 0
+
+
 def _run_pool(job, argsets, workers):
+    """One worker process per GPU (at most `workers`), each pinned to its device; files are handed out one at a
+    time in input order and the results come back in that order."""
     if not argsets:
         return []
+    n_gpus = _gpu_count()
+    procs = max(1, min(workers, len(argsets), n_gpus if n_gpus > 0 else workers))
     ctx = mp.get_context("spawn")
-    with ctx.Pool(processes=min(workers, len(argsets))) as pool:
-        return pool.map(job, argsets)
+    counter = ctx.Value("i", 0)
+    with ctx.Pool(processes=procs, initializer=_pin_device, initargs=(counter, n_gpus)) as pool:
+        return pool.map(job, argsets, chunksize=1)
 
 
 def main(argv=None):
