@@ -65,6 +65,27 @@ __global__ void k_domain_pool(const float* __restrict__ sig, int64_t nd, int rs,
 
 // Embedding of one domain row x[0..rs) read as src[d*a + k*b]; optionally writes the pool row.
 //   tab layout (f64): tonal rows [8][rs] then transient rows [8][rs]; zero rows past take / tk.
+// fp16 copies of embedding row d for the similarity search, tiled [chunk of 256][half h][256][8] (fwav_topk.hip): the
+// high part x_hi = f16(x) (the stream's pre-filter), then, one table further on, the low part x_lo = f16(x − x_hi)
+// (the replay's refined score x_hi·y_hi + x_hi·y_lo + x_lo·y_hi).  Both conversions round to nearest even and keep
+// fp16 subnormals (the hi/lo error bound, DESIGN §3.1, counts on them).
+__device__ __forceinline__ void store_emb16(_Float16* __restrict__ emb16, int64_t nd, int64_t d, const float (&out)[16]) {
+  const int64_t c = d >> 8, j = d & 255;
+  const int64_t n16 = ((nd + 255) >> 8) * 256 * 16;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+    half8 vh, vl;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      vh[e] = (_Float16)out[8 * hh + e];
+      vl[e] = (_Float16)(out[8 * hh + e] - (float)vh[e]);
+    }
+    *reinterpret_cast<half8*>(emb16 + ((c * 2 + hh) * 256 + j) * 8) = vh;
+    *reinterpret_cast<half8*>(emb16 + n16 + ((c * 2 + hh) * 256 + j) * 8) = vl;
+  }
+}
+
 template <int RS>
 __global__ void k_embed(const float* __restrict__ src, int64_t nd, int rs, int64_t a, int64_t b,
                         const double* __restrict__ tab, float* __restrict__ pool_out, float* __restrict__ emb,
@@ -166,25 +187,22 @@ __global__ void k_embed(const float* __restrict__ src, int64_t nd, int rs, int64
   float4* o4 = reinterpret_cast<float4*>(emb + d * 16);
 #pragma unroll
   for (int j = 0; j < 4; ++j) o4[j] = make_float4(out[4 * j], out[4 * j + 1], out[4 * j + 2], out[4 * j + 3]);
-  if (emb16 != nullptr) {
-    // fp16 copies for the similarity search, tiled [chunk of 256][half h][256][8] (fwav_topk.hip): the high part
-    // x_hi = f16(x) (the stream's pre-filter), then, one table further on, the low part x_lo = f16(x − x_hi)
-    // (the replay's refined score x_hi·y_hi + x_hi·y_lo + x_lo·y_hi)
-    const int64_t c = d >> 8, j = d & 255;
-    const int64_t n16 = ((nd + 255) >> 8) * 256 * 16;
+  if (emb16 != nullptr) store_emb16(emb16, nd, d, out);
+}
+
+// Domain-embedding rows → the fp16 tables of the search (store_emb16), for embeddings produced elsewhere.
+__global__ __launch_bounds__(kPoolThreads) void k_emb16(const float* __restrict__ emb, int64_t nd,
+                                                        _Float16* __restrict__ emb16) {
+  const int64_t d = (int64_t)blockIdx.x * kPoolThreads + threadIdx.x;
+  if (d >= nd) return;
+  float out[16];
+  const float4* p = reinterpret_cast<const float4*>(emb + d * 16);
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-      half8 vh, vl;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        vh[e] = (_Float16)out[8 * hh + e];
-        vl[e] = (_Float16)(out[8 * hh + e] - (float)vh[e]);
-      }
-      *reinterpret_cast<half8*>(emb16 + ((c * 2 + hh) * 256 + j) * 8) = vh;
-      *reinterpret_cast<half8*>(emb16 + n16 + ((c * 2 + hh) * 256 + j) * 8) = vl;
-    }
+  for (int j = 0; j < 4; ++j) {
+    const float4 v = p[j];
+    out[4 * j] = v.x; out[4 * j + 1] = v.y; out[4 * j + 2] = v.z; out[4 * j + 3] = v.w;
   }
+  store_emb16(emb16, nd, d, out);
 }
 
 template <int RS>
@@ -340,6 +358,24 @@ size_t fwav_pool_workspace_size(int64_t n, int tile, int rs, int step) {
 // Domain pool + embedding.  pool: f32[nd*rs], emb: f32[nd*16], tab: device copy of fwav_embed_tables(rs).
 // emb16 (optional): fp16 high and low parts in the tiled layout the similarity search streams,
 // f16[fwav_emb16_elems(nd)] = 2 tables of ceil(nd/256)*256*16; rows past nd are zeroed here.
+// fp16 search tables (f16[fwav_emb16_elems(nd)]) of embedding rows emb f32[nd*16], as fwav_pool_embed writes them.
+int fwav_emb16_from_emb(const float* emb, int64_t nd, void* emb16, void* stream) {
+  FWAV_CHECK_ARG(emb && emb16 && nd > 0, FWAV_ERR_ARG, "fwav_emb16_from_emb: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  _Float16* e16 = (_Float16*)emb16;
+  if ((nd & 255) != 0) {
+    const int64_t c = nd >> 8, j0 = nd & 255;
+    const int64_t n16 = ((nd + 255) >> 8) * 256 * 16;
+    for (int tb = 0; tb < 2; ++tb)
+      for (int hh = 0; hh < 2; ++hh)
+        (void)hipMemsetAsync(e16 + tb * n16 + ((c * 2 + hh) * 256 + j0) * 8, 0,
+                             (size_t)(256 - j0) * 8 * sizeof(_Float16), st);
+  }
+  k_emb16<<<cdiv(nd, kPoolThreads), kPoolThreads, 0, st>>>(emb, nd, e16);
+  FWAV_LAUNCH_CHECK("fwav_emb16_from_emb");
+  return FWAV_OK;
+}
+
 int fwav_pool_embed(const float* sig, int64_t n, int tile, int rs, int step, const double* tab, float* pool,
                     float* emb, void* emb16, void* workspace, size_t ws_bytes, void* stream) {
   FWAV_CHECK_ARG(sig && pool && emb && tab && tile > 0 && rs > 0 && step > 0, FWAV_ERR_ARG,

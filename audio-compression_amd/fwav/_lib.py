@@ -51,6 +51,7 @@ SIGNATURES = {
     "fwav_affine": (I32, [P, I64, I32, P, I32, P, I64, F32, P, P, P, P, P, P]),
     "fwav_tie_check": (I32, [P, I64, I32, P, I32, P, I64, P, I64, I32, P, I64, I32, P, P]),
     "fwav_tie_list_size": (I64, [I64]),
+    "fwav_emb16_from_emb": (I32, [P, I64, P, P]),
     "fwav_debug_topk_plan_info": (I32, [I64, I64, P, P]),
     "fwav_decode_workspace_size": (SZ, [I64, I32, I32]),
     "fwav_decode": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, SZ, P]),

@@ -70,6 +70,9 @@ int fwav_debug_smooth(const float* energy, int64_t nf, int smooth_window, float*
  * n_domains = (n − tile) / step + 1.  tab = device copy of fwav_embed_tables(range_size) (host call, tab_host holds
  * fwav_embed_tables_size(range_size) doubles). */
 size_t fwav_emb16_elems(int64_t n_domains);
+/* The fp16 search tables (hi/lo parts, f16[fwav_emb16_elems(n_domains)]) of embedding rows emb f32[n_domains·16],
+ * exactly as fwav_pool_embed writes them — for embeddings that did not come from fwav_pool_embed (tests). */
+int fwav_emb16_from_emb(const float* emb, int64_t n_domains, void* emb16, void* stream);
 size_t fwav_embed_tables_size(int range_size);
 int fwav_embed_tables(int range_size, double* tab_host);
 /* Test hook (host, no device): scipy.fftpack.dct(x, norm='ortho') for n = 4, 8, 16 in float32 (dbl = 0) or float64

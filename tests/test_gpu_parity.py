@@ -398,3 +398,55 @@ def test_half_of_41344_queries_pieces_plan_stays_in_workspace():
         assert ((c >= 0) & (c < nd)).all()
         out.append(c)
     assert np.array_equal(out[0], out[1])
+
+
+def _adversarial_emb(nd, seed):
+    """Unit-head embedding rows built to stress the fp16 hi/lo split (DESIGN §3.1 δ′ bound): components exactly
+    halfway between fp16 neighbours (x_hi rounds to even, x_lo is a whole half-ulp), components below 2^-14 (fp16
+    subnormal x_hi) and below 2^-3 (fp16-subnormal x_lo); heads brought to norm ≤ 1 by exact halvings; every third
+    row a near-duplicate of another (one component moved by one fp16 ulp), which packs scores near the K-th."""
+    rng = np.random.default_rng(seed)
+    E = np.empty((nd, 16), np.float32)
+    j = np.arange(8)
+    for h in (0, 1):
+        kind = rng.integers(0, 3, nd)[:, None]
+        mant = rng.integers(0, 1024, (nd, 8))
+        mid = np.ldexp(1024.0 + mant + 0.5, rng.integers(-6, 0, (nd, 8)) - 10)
+        tiny = np.where(j % 2 == 1, np.ldexp(1.0 + rng.random((nd, 8)), -15 - (j % 9)), np.ldexp(1024.0 + mant + 0.5, -11))
+        small = np.ldexp(rng.random((nd, 8)), -4 - (j % 3))
+        x = np.where(kind == 0, mid, np.where(kind == 1, tiny, small)) * np.where(rng.random((nd, 8)) < 0.5, -1.0, 1.0)
+        k = np.maximum(0, np.ceil(np.log2(np.maximum((x * x).sum(1), 1e-300)) / 2)).astype(np.int64)
+        E[:, 8 * h:8 * h + 8] = np.ldexp(x, -k[:, None]).astype(np.float32)
+    dup = np.arange(0, nd, 3)
+    E[dup] = E[rng.integers(0, nd, len(dup))]
+    E[dup, rng.integers(0, 16, len(dup))] *= np.float32(0.99951171875)
+    assert (np.sqrt((E[:, :8].astype(np.float64) ** 2).sum(1)) <= 1).all()
+    assert (np.sqrt((E[:, 8:].astype(np.float64) ** 2).sum(1)) <= 1).all()
+    return E
+
+
+@pytest.mark.parametrize("K", [64, 17])
+def test_hilo_band_adversarial_embeddings(K, first_mode):
+    """The fp16 search in every first-pass mode (the hi/lo band above all) returns the all-f32 kernel's candidates on
+    embeddings built to break the hi/lo error bound (fp16 midpoints, fp16-subnormal hi and lo parts, near-duplicate
+    rows): the band margins δ = 2e-3 / δ′ = 1e-5 hold there too."""
+    from fwav._lib import size_call
+    nd, nq = 60_000, 4096
+    E = _adversarial_emb(nd, 7)
+    emb = td(E.reshape(-1))
+    st = torch.cuda.current_stream().cuda_stream
+    emb16 = torch.empty(size_call("fwav_emb16_elems", nd), dtype=torch.float16, device=dev())
+    call("fwav_emb16_from_emb", emb.data_ptr(), nd, emb16.data_ptr(), st)
+    act = torch.arange(nq, dtype=torch.int32, device=dev())
+    n_act = torch.tensor([nq], dtype=torch.int32, device=dev())
+    out = []
+    for e16 in (emb16.data_ptr(), None):
+        wsn = size_call("fwav_sim_topk_workspace_size", nq, nd, K)
+        wsk = torch.empty(max(wsn, 16), dtype=torch.uint8, device=dev())
+        cand = torch.full((nq * K,), -7, dtype=torch.int32, device=dev())
+        call("fwav_sim_topk", emb.data_ptr(), e16, nd, act.data_ptr(), n_act.data_ptr(), nq, 0, K, 1,
+             cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
+        torch.cuda.synchronize()
+        out.append(cand.view(nq, K).cpu().numpy())
+    assert ((out[1] >= 0) & (out[1] < nd)).all()
+    assert np.array_equal(out[0], out[1])

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <random>
+#include <string>
 #include <vector>
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -40,7 +41,55 @@ static float sgemv(const float* q, const float* d) {
   return (r[0] + r[1]) + (r[2] + r[3]);
 }
 
-int main() {
+__global__ void k_denorm(float* out) {
+  // one MFMA whose only non-zero products are fp16 subnormals: 2^-24 · 1 and (3·2^-24) · 0.5
+  const int lane = threadIdx.x & 63;
+  half8 a{}, b{};
+  if (lane == 0) { a[0] = (_Float16)5.9604645e-8f; a[1] = (_Float16)1.7881393e-7f; }
+  if (lane == 0) { b[0] = (_Float16)1.0f; b[1] = (_Float16)0.5f; }
+  const floatx16 r = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, floatx16{}, 0, 0, 0);
+  if (lane == 0) out[0] = r[0];
+}
+
+// Adversarial unit-head vectors (argv[1] == "adv"): components exactly halfway between fp16 neighbours (the hi
+// split rounds to even, the lo part is a whole half-ulp), components below 2^-14 (fp16-subnormal hi parts) and
+// below 2^-3 (fp16-subnormal lo parts); heads scaled by powers of two only, so the constructions stay exact.
+static void adversarial(float* v, std::mt19937& g) {
+  std::uniform_int_distribution<int> mant(0, 1023), ex(-6, -1), kind(0, 3), sgn(0, 1);
+  std::uniform_real_distribution<float> u(0.f, 1.f);
+  for (int hh = 0; hh < 2; ++hh) {
+    const int kd = kind(g);
+    for (int j = 0; j < 8; ++j) {
+      float x;
+      if (kd == 0 || (kd == 3 && j < 4)) {
+        x = std::ldexp((float)(1024 + mant(g)) + 0.5f, ex(g) - 10);  // fp16 midpoint
+      } else if (kd == 1) {
+        x = (j % 2) ? std::ldexp(1.f + u(g), -15 - (j % 9)) : std::ldexp((float)(1024 + mant(g)) + 0.5f, -11);
+      } else {
+        x = std::ldexp(u(g), -4 - (j % 3));  // < 2^-3: fp16-subnormal lo parts
+      }
+      v[8 * hh + j] = sgn(g) ? -x : x;
+    }
+    for (;;) {  // norm ≤ 1 by exact halvings
+      double s = 0;
+      for (int j = 0; j < 8; ++j) s += (double)v[8 * hh + j] * v[8 * hh + j];
+      if (s <= 1.0) break;
+      for (int j = 0; j < 8; ++j) v[8 * hh + j] *= 0.5f;
+    }
+  }
+}
+
+int main(int argc, char** argv) {
+  const bool adv = argc > 1 && std::string(argv[1]) == "adv";
+  {
+    float* dout;
+    hipMalloc(&dout, 4);
+    k_denorm<<<1, 64>>>(dout);
+    float r = 0;
+    hipMemcpy(&r, dout, 4, hipMemcpyDeviceToHost);
+    std::printf("fp16-subnormal MFMA products: %.9g (expected %.9g: %s)\n", r, 5.9604645e-8 + 0.5 * 1.7881393e-7,
+                r == (float)(5.9604645e-8 + 0.5 * 1.7881393e-7) ? "kept" : "FLUSHED");
+  }
   const int N = 32 * 8192;
   std::mt19937 g(1);
   std::normal_distribution<float> nrm(0.f, 1.f);
@@ -54,10 +103,18 @@ int main() {
   };
   std::vector<float> Q(32 * 16), D((size_t)N * 16);
   for (auto& x : Q) x = nrm(g);
-  for (int i = 0; i < 32; ++i) unit_heads(&Q[i * 16]);
+  for (int i = 0; i < 32; ++i) {
+    if (adv) adversarial(&Q[i * 16], g); else unit_heads(&Q[i * 16]);
+  }
   for (int i = 0; i < N; ++i) {
     float* v = &D[(size_t)i * 16];
     const bool dup = (i % 3) == 0;
+    if (adv) {
+      adversarial(v, g);
+      if (dup)  // the query itself with one component moved to a neighbouring fp16 midpoint
+        for (int j = 0; j < 16; ++j) v[j] = Q[(i % 32) * 16 + j] * ((j == i % 16) ? 0.99951171875f : 1.f);
+      continue;
+    }
     const float eps = (i % 7) * 1e-3f;
     for (int j = 0; j < 16; ++j) v[j] = dup ? Q[(i % 32) * 16 + j] + eps * nrm(g) : nrm(g);
     if ((i % 11) == 0)  // small magnitudes (fp16 subnormal lo parts)
