@@ -46,7 +46,7 @@ def test_bindings_match_header(lib):
 
 def test_error_codes_without_gpu(lib):
     L = lib.lib()
-    assert L.fwav_abi_version() == 3
+    assert L.fwav_abi_version() == 4
     rc = L.fwav_affine(None, 10, 8, None, 64, None, 100, 16.0, None, None, None, None, None, None)
     assert rc == -1 and b"null" in L.fwav_last_error()
     rc = L.fwav_sim_topk(None, None, 10, None, None, 10, 0, 64, 1, None, None, None, 0, None)
