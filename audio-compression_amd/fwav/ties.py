@@ -19,6 +19,7 @@ the device; numpy only orders equal keys, exactly as it does in the reference.
 from __future__ import annotations
 
 import os
+import time
 
 import numpy as np
 import torch
@@ -85,6 +86,8 @@ def defer(finish, device: torch.device):
     ev.record(torch.cuda.current_stream(device))
     key = str(device)
     if key not in _SIDE:
+        # (a high-priority stream was measured no better: its kernels still wait behind the next call's search,
+        # which holds every CU — profiles/r03/ties_defer_cfg3.log)
         _SIDE[key] = torch.cuda.Stream(device)
     side = _SIDE[key]
 
@@ -128,6 +131,9 @@ def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_off
     n = rows.numel()
     if n == 0:
         return
+    trace = os.environ.get("FWAV_TIES_TRACE")
+    t0 = time.perf_counter()
+    tw = 0.0
     nd = int(n_domains)
     per = max(1, min(n, ROW_BUDGET // (4 * nd)))
     cv = cand.view(-1, k)
@@ -147,12 +153,18 @@ def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_off
         h = _pinned(bi & 1, m * nd)
         h.copy_(S[:m * nd], non_blocking=True)
         ev[bi & 1].record()
+        tw0 = time.perf_counter()
         ev[bi & 1].synchronize()  # S is reused by the next batch and h is read by the threads
+        tw += time.perf_counter() - tw0
         Sh = h.numpy().reshape(m, nd)
         batch = [ex.submit(numpy_topk_row, Sh[i], k) for i in range(m)]
         staged.append(batch)
         futs.extend(batch)
+    t1 = time.perf_counter()
     newc = torch.from_numpy(np.stack([f.result() for f in futs])).to(dev)
+    if trace:
+        print(f"fwav.ties: {n} rows x {nd}: {(time.perf_counter() - t0) * 1e3:.1f} ms (device score rows + copies "
+              f"waited {tw * 1e3:.1f} ms, numpy tail {(time.perf_counter() - t1) * 1e3:.1f} ms)", flush=True)
     ridx = rows.long()
     cv[ridx] = newc
     rs = int(range_size)
