@@ -450,3 +450,24 @@ def test_hilo_band_adversarial_embeddings(K, first_mode):
         out.append(cand.view(nq, K).cpu().numpy())
     assert ((out[1] >= 0) & (out[1] < nd)).all()
     assert np.array_equal(out[0], out[1])
+
+
+def test_deferred_tie_resolution_equals_synchronous():
+    """defer_ties=True (the bench's pipelined mode): the host half of the tie resolution runs on the driver thread
+    while later calls are queued; after wait() every output equals the synchronous call's, for several calls in
+    flight at once (tone, K = 32: its byte-identical tiles give rows that numpy re-ranks)."""
+    g = load("tone")
+    p = g["p"]
+    sig = td(g["signal"])
+    ref = engine.compress_device(sig, p["tile"], 32, energy_thresh=p["thr"], keep_intermediates=True)
+    torch.cuda.synchronize()
+    assert ref.n_resolved > 0
+    outs = [engine.compress_device(sig, p["tile"], 32, energy_thresh=p["thr"], keep_intermediates=True,
+                                   defer_ties=True) for _ in range(3)]
+    for r in outs:
+        r.wait()
+    torch.cuda.synchronize()
+    for r in outs:
+        assert (r.n_ties, r.n_resolved) == (ref.n_ties, ref.n_resolved)
+        for nm in ("cand", "idx", "s", "o", "sym", "err"):
+            assert bit_equal(getattr(r, nm).cpu().numpy(), getattr(ref, nm).cpu().numpy()), nm
