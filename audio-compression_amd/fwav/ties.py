@@ -26,8 +26,10 @@ import torch
 
 from ._lib import call
 
-#: host bytes of exact score rows fetched per batch
-ROW_BUDGET = 256 << 20
+#: device bytes of exact score rows computed per fwav_score_rows launch (the launch reads the embedding table once)
+DEVICE_ROW_BUDGET = 2 << 30
+#: page-locked host bytes of score rows in flight (one slot per row being ranked)
+HOST_ROW_BUDGET = 4 << 30
 
 _BLAS_THREADS = None
 
@@ -69,7 +71,7 @@ def numpy_topk_row(scores: np.ndarray, k: int) -> np.ndarray:
 
 
 _POOL = None
-_PINNED: dict = {}
+_SLOTS: list = []
 _DRIVER = None
 _SIDE: dict = {}
 
@@ -101,32 +103,36 @@ def defer(finish, device: torch.device):
 
 
 def _pool():
-    """Host threads for numpy's ranking of the exact score rows (argpartition runs outside the GIL; the box's 16-CPU
-    share: 8 threads measured 5.7x one at cfg2 row widths, profiles/r03/host_tie_cost.log)."""
+    """Host threads for numpy's ranking of the exact score rows (argpartition runs outside the GIL; measured on the
+    box's 16-CPU share: 8 threads 5.7x one at cfg2 row widths, `profiles/r03/host_tie_cost.log`)."""
     global _POOL
     if _POOL is None:
         from concurrent.futures import ThreadPoolExecutor
-        n = int(os.environ.get("FWAV_TIE_THREADS", "8"))
+        n = int(os.environ.get("FWAV_TIE_THREADS", str(min(8, os.cpu_count() or 1))))
         _POOL = ThreadPoolExecutor(max(1, n), thread_name_prefix="fwav-ties")
     return _POOL
 
 
-def _pinned(slot: int, numel: int) -> torch.Tensor:
-    """A reusable page-locked staging buffer (float32), one per double-buffer slot."""
-    t = _PINNED.get(slot)
+def _slot(i: int, numel: int) -> torch.Tensor:
+    """Reusable page-locked staging row i (float32), grown on demand."""
+    while len(_SLOTS) <= i:
+        _SLOTS.append(None)
+    t = _SLOTS[i]
     if t is None or t.numel() < numel:
         t = torch.empty(numel, dtype=torch.float32, pin_memory=True)
-        _PINNED[slot] = t
+        _SLOTS[i] = t
     return t[:numel]
 
 
 def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, k: int, threads: int,
                  ranges: torch.Tensor, range_size: int, pool: torch.Tensor, s_clip: float, cand: torch.Tensor,
                  outs: tuple, stream: int) -> None:
-    """Rows (local indices, device int32) whose match depends on numpy's tie order: exact score rows in batches
-    (fwav_score_rows, copied to page-locked memory while the host ranks the previous batch), numpy's ranking of each
-    row on a host thread pool, the new candidate rows written back to ``cand`` and the affine solve re-run for those
-    rows into ``outs`` = (idx, s, o, sym, err)."""
+    """Rows (local indices, device int32) whose match depends on numpy's tie order: exact score rows in launches of up
+    to DEVICE_ROW_BUDGET (fwav_score_rows reads the embedding table once per launch), copied to a ring of page-locked
+    row slots (HOST_ROW_BUDGET), numpy's ranking of each row on a host thread pool as soon as it lands, the new
+    candidate rows written back to ``cand`` and the affine solve re-run for those rows into ``outs`` =
+    (idx, s, o, sym, err).  (cfg4-sized rows, 86.4 M scores: 22 rows 3.5 → 1.1 s against one 256 MB
+    double buffer.)"""
     dev = rows.device
     n = rows.numel()
     if n == 0:
@@ -135,31 +141,36 @@ def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_off
     t0 = time.perf_counter()
     tw = 0.0
     nd = int(n_domains)
-    per = max(1, min(n, ROW_BUDGET // (4 * nd)))
+    per = max(1, min(n, DEVICE_ROW_BUDGET // (4 * nd)))     # rows per fwav_score_rows launch
+    nslots = max(2, min(n, HOST_ROW_BUDGET // (4 * nd)))   # rows staged on the host at once
     cv = cand.view(-1, k)
     ex = _pool()
-    futs = []
+    futs = [None] * n
+    slot_busy = [None] * nslots  # the future ranking each slot's row
     S = torch.empty(per * nd, dtype=torch.float32, device=dev)
-    ev = [torch.cuda.Event(), torch.cuda.Event()]
-    staged = []
-    for bi, b0 in enumerate(range(0, n, per)):
+    ev = torch.cuda.Event()
+    for b0 in range(0, n, per):
         rb = rows[b0:b0 + per].contiguous()
         m = rb.numel()
-        if bi >= 2:  # the staging slot about to be overwritten: its rows are ranked already
-            for f in staged[bi - 2]:
-                f.result()
         call("fwav_score_rows", emb.data_ptr(), nd, rb.data_ptr(), m, int(q_offset), int(threads), S.data_ptr(),
              stream)
-        h = _pinned(bi & 1, m * nd)
-        h.copy_(S[:m * nd], non_blocking=True)
-        ev[bi & 1].record()
-        tw0 = time.perf_counter()
-        ev[bi & 1].synchronize()  # S is reused by the next batch and h is read by the threads
-        tw += time.perf_counter() - tw0
-        Sh = h.numpy().reshape(m, nd)
-        batch = [ex.submit(numpy_topk_row, Sh[i], k) for i in range(m)]
-        staged.append(batch)
-        futs.extend(batch)
+        # copy the launch's rows to free staging slots in runs of at most nslots, one synchronisation per run
+        for r0 in range(0, m, nslots):
+            run = range(b0 + r0, b0 + min(m, r0 + nslots))
+            hs = []
+            for i in run:
+                sl = i % nslots
+                if slot_busy[sl] is not None:  # its previous row is still being ranked
+                    slot_busy[sl].result()
+                h = _slot(sl, nd)
+                h.copy_(S[(i - b0) * nd:(i - b0 + 1) * nd], non_blocking=True)
+                hs.append((i, sl, h))
+            ev.record()
+            tw0 = time.perf_counter()
+            ev.synchronize()
+            tw += time.perf_counter() - tw0
+            for i, sl, h in hs:
+                futs[i] = slot_busy[sl] = ex.submit(numpy_topk_row, h.numpy(), k)
     t1 = time.perf_counter()
     newc = torch.from_numpy(np.stack([f.result() for f in futs])).to(dev)
     if trace:

@@ -57,7 +57,8 @@ def main():
         st = {k: v[0].elapsed_time(v[1]) for k, v in ev.items()}
         na = int(res.n_active.item())
         fl = 2.0 * na * res.n_domains * 16
-        out[f"rep{rep}"] = {"wall_s": wall, "stage_ms": st, "active_queries": na,
+        out[f"rep{rep}"] = {"wall_s": wall, "stage_ms": st, "active_queries": na, "n_ties": res.n_ties,
+                            "n_resolved": res.n_resolved,
                             "sim_topk_tflops": fl / (st["sim_topk"] * 1e-3) / 1e12,
                             "sim_topk_frac_f16_peak": fl / (st["sim_topk"] * 1e-3) / 1e12 / F16_PEAK,
                             "full_cfg4_search_s_extrapolated": st["sim_topk"] * 1e-3 * res.n_ranges / q}
