@@ -133,7 +133,20 @@ def compress_sharded_device(sig: Optional[torch.Tensor], tile_size: int, top_k: 
     Returns on rank 0 a dict of full-length device tensors idx/s/o/sym/err, the pool, the blocks and geometry;
     None on the other ranks.  ``n`` (the signal length, if every rank knows it) saves broadcasting it.
     ``timings`` (if given) receives per-phase host seconds (broadcast / compute / gather), each phase then closed by
-    a device synchronisation (without it the phases run back to back, with no synchronisation of their own)."""
+    a device synchronisation (without it the phases run back to back, with no synchronisation of their own).
+    Equal to ``compress_sharded_finish(compress_sharded_start(...))``."""
+    return compress_sharded_finish(compress_sharded_start(sig, tile_size, top_k, energy_thresh, group, device, compute,
+                                                          timings, n))
+
+
+def compress_sharded_start(sig: Optional[torch.Tensor], tile_size: int, top_k: int, energy_thresh: float = 1e-4,
+                           group=None, device: Optional[torch.device] = None, compute: Optional[Callable] = None,
+                           timings: Optional[dict] = None, n: Optional[int] = None) -> dict:
+    """First half of :func:`compress_sharded_device`: the signal broadcast and this rank's search + solve, queued.
+    ``compute`` may return a ``wait`` callable (a deferred tie resolution, engine.compress_device(defer_ties=True));
+    :func:`compress_sharded_finish` calls it before the gather.  A stream of calls can keep a few started calls in
+    flight and finish them in order, so that one call's host tie ranking overlaps the next calls' searches (bench.py);
+    every rank must start and finish the same calls in the same order (the collectives pair up by order)."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     if device is None:
@@ -160,7 +173,6 @@ def compress_sharded_device(sig: Optional[torch.Tensor], tile_size: int, top_k: 
     t1 = mark()
 
     rs, step = geometry(tile_size)
-    nr = -(-n // rs)
     blocks_box: list = []
 
     def shard(ranges, n_ranges, range_size):
@@ -168,13 +180,26 @@ def compress_sharded_device(sig: Optional[torch.Tensor], tile_size: int, top_k: 
         return blocks_box[rank]
 
     res = compute(sig, tile_size, top_k, energy_thresh, shard)
+    return dict(rank=rank, world=world, group=group, device=device, res=res, blocks=blocks_box, n=n, rs=rs,
+                step=step, tm=tm, mark=mark, t=[t0, t1])
+
+
+def compress_sharded_finish(h: dict):
+    """Second half of :func:`compress_sharded_device` for a handle from :func:`compress_sharded_start`: completes a
+    deferred tie resolution, then gathers the match arrays to rank 0."""
+    res, tm, mark = h["res"], h["tm"], h["mark"]
+    t0, t1 = h["t"]
+    rank, world, group, n, rs, step = h["rank"], h["world"], h["group"], h["n"], h["rs"], h["step"]
+    if res is not None and res.get("wait") is not None:
+        res["wait"]()
     t2 = mark()
     if res is None:  # empty / short / silent input: identical decision on every rank
         tm.update(broadcast_s=t1 - t0, compute_s=t2 - t1, gather_s=0.0)
         return dict(empty=True, n_ranges=0, range_size=rs, domain_step=step, original_len=n) if rank == 0 else None
-    blocks = blocks_box
+    nr = -(-n // rs)
+    blocks = h["blocks"]
     maxlen = max(1, max(b - a for a, b in blocks))
-    cd = _coll_device(group, device)
+    cd = _coll_device(group, h["device"])
     mine = _pack(res, maxlen, cd)
     glist = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
     dist.gather(mine, gather_list=glist, dst=0, group=group)

@@ -8,9 +8,10 @@ mirror, all on device; the signal is resident in HBM before the timed region and
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N) runs the north star's sharded
 path on the same single signal (strong scaling, "scaling": "strong"): rank 0 holds the signal in HBM, RCCL
 broadcasts it over xGMI, every rank rebuilds ranges/pool/embeddings, searches + solves its prune-balanced block of
-ranges, and the match arrays are gathered to rank 0 (fwav.dist.compress_sharded_device).  The timed step
-includes the broadcast and the gather; value = n_ranges / max-over-ranks step time.  N = 1 is the same path with
-no collective (compress_device), so the driver's per-N values form a strong-scaling curve.
+ranges, and the match arrays are gathered to rank 0 (fwav.dist.compress_sharded_start/finish).  The timed steps
+include every broadcast and gather; up to two calls are in flight, so a call's host tie ranking (defer_ties, as
+at N = 1) overlaps the next calls' searches before its gather; value = n_ranges / max-over-ranks step time.  N = 1
+is the same path with no collective (compress_device), so the driver's per-N values form a strong-scaling curve.
 
 Also reported: the dominant kernel's roofline (similarity top-K vs the fp16 MFMA peak; HIP events on the launch
 stream; `traffic` = PMC bytes from a committed rocprofv3 pass of the same config, labelled with its source), the
@@ -194,21 +195,32 @@ def main():
             step.pending.append(r)
             return r
     else:
+        LAG = 2  # started calls in flight before the oldest is finished (its ties waited for, its matches gathered)
+
         def step(ev=None, phases=False):
             def compute(s, t, k, thr, shard):
-                r = engine.compress_device(s, t, k, energy_thresh=thr, shard=shard, events=ev)
+                r = engine.compress_device(s, t, k, energy_thresh=thr, shard=shard, events=ev, defer_ties=not phases)
                 step.last = r
                 return None if r.empty else dict(idx=r.idx, s=r.s, o=r.o, sym=r.sym, err=r.err, pool=r.pool,
-                                                 silent=r.is_silent)
+                                                 silent=r.is_silent, wait=r.wait)
             # every rank knows the configuration's signal length; per-phase host timings (which synchronise the
-            # device at each phase boundary) are taken on an extra step after the timed ones
+            # device at each phase boundary) are taken on extra unpipelined steps after the timed ones
             tm = {} if phases else None
-            out = fdist.compress_sharded_device(sig, tile, K, 1e-4, device=dev, compute=compute, timings=tm,
-                                                n=int(sig_h.size))
-            for k_, v in (tm or {}).items():
-                phase.setdefault(k_, []).append(v)
-            step.out = out
+            h = fdist.compress_sharded_start(sig, tile, K, 1e-4, device=dev, compute=compute, timings=tm,
+                                             n=int(sig_h.size))
+            if phases:
+                step.out = fdist.compress_sharded_finish(h)
+                for k_, v in tm.items():
+                    phase.setdefault(k_, []).append(v)
+            else:
+                # like N = 1's deferred ties: a call's host tie ranking overlaps the next calls' searches, and its
+                # gather follows once it is final; every started call is finished inside the timed region (drain)
+                step.inflight.append(h)
+                while len(step.inflight) > LAG:
+                    step.out = fdist.compress_sharded_finish(step.inflight.pop(0))
             return step.last
+
+        step.inflight = []
 
     if world == 1:
         step.pending = []
@@ -218,6 +230,8 @@ def main():
             r.wait()
         if world == 1:
             step.pending = []
+        while getattr(step, "inflight", None):
+            step.out = fdist.compress_sharded_finish(step.inflight.pop(0))
 
     for _ in range(args.warmup):
         res = step()

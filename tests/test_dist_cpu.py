@@ -87,6 +87,78 @@ def test_sharded_equals_single_process(world):
     assert all(blocks[i][1] == blocks[i + 1][0] for i in range(world - 1))
 
 
+def _pipelined_worker(rank, world, port, sigs, tile, k, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "audio-compression_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from fwav.dist import compress_sharded_finish, compress_sharded_start
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    waited = []
+
+    def compute(sig, tile_size, top_k, thr, shard):
+        r = _oracle_compute(sig, tile_size, top_k, thr, shard)
+        tag = len(waited)
+        waited.append(False)
+        # a deferred result: err is only final once wait() ran (as with engine.compress_device(defer_ties=True))
+        final = r["err"].clone()
+        r["err"] = torch.full_like(final, float("nan"))
+
+        def wait():
+            r["err"].copy_(final)
+            waited[tag] = True
+        r["wait"] = wait
+        return r
+
+    outs, inflight = [], []
+    for sg in sigs:  # two calls in flight, finished in order (bench.py's multi-rank timed loop)
+        inflight.append(compress_sharded_start(torch.from_numpy(sg) if rank == 0 else None, tile, k, 1e-4,
+                                               device=torch.device("cpu"), compute=compute, n=len(sg)))
+        while len(inflight) > 2:
+            outs.append(compress_sharded_finish(inflight.pop(0)))
+    outs += [compress_sharded_finish(h) for h in inflight]
+    if rank == 0:
+        q.put(dict(outs=[{kk: np.asarray(v) for kk, v in o.items() if kk in ("idx", "s", "o", "sym", "err")}
+                         for o in outs], waited=waited))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_pipelined_start_finish_equals_single_process():
+    """compress_sharded_start/finish with two calls in flight: each call's gathered arrays equal a single-process
+    run on its own signal, and each deferred result was completed before its gather."""
+    from fwav import synth
+    from oracle import fractal_oracle as O
+    sigs = [synth.speech_like(0.6, 16000, seed=s, floor=False) for s in (3, 4, 5, 6)]
+    tile, k, world = 1024, 8, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, sigs, tile, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = None
+    import queue as _q
+    for _ in range(240):
+        try:
+            out = q.get(timeout=1)
+            break
+        except _q.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        p.join(timeout=60)
+        if p.exitcode is None:
+            p.kill()
+    assert out is not None, "a rank failed"
+    assert all(p.exitcode == 0 for p in procs)
+    assert out["waited"] == [True] * len(sigs)
+    assert len(out["outs"]) == len(sigs)
+    for sg, got in zip(sigs, out["outs"]):
+        ref = O.compress(sg, tile, k)
+        for f in ("idx", "s", "o", "sym", "err"):
+            assert np.array_equal(got[f].view(np.uint8), np.asarray(ref[f]).view(np.uint8)), f
+
+
 def test_balanced_bounds():
     from fwav.dist import balanced_bounds
     w = np.r_[np.zeros(1000), np.ones(1000), np.zeros(500), np.ones(1000)]

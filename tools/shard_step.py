@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """One rank's share of the sharded cfg2 compress, on one GPU (diagnostic for strong scaling): the step time of
-compress_device(sig, shard=(0, nr/N)) for N = 1, 2, 4, 8 — everything a rank of bench.py --gpus N does except the
-collectives — with per-stage HIP events and the host wall time per step.
+compress_device(sig, shard=block r of N) for N = 1, 2, 4, 8 and every rank r — everything a rank of bench.py --gpus N
+does except the collectives — with per-stage HIP events and the host wall time per step, ties resolved synchronously
+("sync") and deferred with two calls in flight as bench.py's timed loop runs them ("pipelined").  The slowest rank
+sets the step time.
 usage: python tools/shard_step.py [--steps 20]"""
 from __future__ import annotations
 
@@ -34,26 +36,41 @@ def main():
     tile, K = cfg["tile"], cfg["top_k"]
     out = {}
     for N in (1, 2, 4, 8):
-        def shard(ranges, n_ranges, range_size, N=N):
-            return fdist.prune_balanced_bounds(ranges, n_ranges, range_size, 1e-4, N)[0]
-        for _ in range(2):
-            engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard)
-        torch.cuda.synchronize()
-        evs = []
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            ev = {}
-            r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard, events=ev)
-            evs.append(ev)
-        torch.cuda.synchronize()
-        wall = (time.perf_counter() - t0) / a.steps * 1e3
-        st = {k: float(np.mean([e[k][0].elapsed_time(e[k][1]) for e in evs])) for k in evs[0]}
-        out[N] = {"ranges": r.shard[1] - r.shard[0], "wall_ms": wall, "stage_ms": st,
-                  "gpu_sum_ms": sum(st.values())}
+        per = []
+        for rank in range(N):
+            def shard(ranges, n_ranges, range_size, N=N, rank=rank):
+                return fdist.prune_balanced_bounds(ranges, n_ranges, range_size, 1e-4, N)[rank]
+            for _ in range(2):
+                engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard)
+            torch.cuda.synchronize()
+            evs = []
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                ev = {}
+                r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard, events=ev)
+                evs.append(ev)
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - t0) / a.steps * 1e3
+            st = {k: float(np.mean([e[k][0].elapsed_time(e[k][1]) for e in evs])) for k in evs[0]}
+            inflight = []
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                inflight.append(engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard,
+                                                       defer_ties=True))
+                while len(inflight) > 2:
+                    inflight.pop(0).wait()
+            for x in inflight:
+                x.wait()
+            torch.cuda.synchronize()
+            pipe = (time.perf_counter() - t0) / a.steps * 1e3
+            per.append({"rank": rank, "ranges": r.shard[1] - r.shard[0], "tie_rows": r.n_resolved,
+                        "wall_ms_sync": wall, "wall_ms_pipelined": pipe, "stage_ms": st})
+        out[N] = {"max_wall_ms_sync": max(p["wall_ms_sync"] for p in per),
+                  "max_wall_ms_pipelined": max(p["wall_ms_pipelined"] for p in per), "ranks": per}
         print(N, json.dumps(out[N]), flush=True)
-    base = out[1]["wall_ms"]
-    print(json.dumps({N: {"speedup_wall": base / v["wall_ms"]} for N, v in out.items()}), flush=True)
-
+    print(json.dumps({N: {"speedup_sync": out[1]["max_wall_ms_sync"] / v["max_wall_ms_sync"],
+                          "speedup_pipelined": out[1]["max_wall_ms_pipelined"] / v["max_wall_ms_pipelined"]}
+                      for N, v in out.items()}), flush=True)
 
 if __name__ == "__main__":
     main()
