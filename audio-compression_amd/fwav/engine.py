@@ -168,7 +168,8 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
                      fast_mode: bool = True, s_clip: float = 16.0, shard: Optional[tuple[int, int]] = None,
                      keep_intermediates: bool = False, events: Optional[dict] = None,
                      search: str = "f16", on_pool=None, blas_threads: Optional[int] = None,
-                     tie_order: str = "numpy", defer_ties: bool = False) -> DeviceCompressed:
+                     tie_order: str = "numpy", defer_ties: bool = False,
+                     sub_blocks: Optional[int] = None) -> DeviceCompressed:
     """Run the compress hot path on ``sig`` (1-D float32 tensor on a HIP device).
 
     ``shard=(lo, hi)`` restricts candidate search and the affine solve to ranges ``[lo, hi)`` (the
@@ -185,7 +186,9 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     the candidate sets are the reference's too; ``"index"`` keeps the device's (score desc, index asc) order (no
     synchronisation).  ``defer_ties=True`` hands that host step to a background thread (its device work on a side
     stream, after this call's kernels) and returns at once: the outputs are final after ``result.wait()``, so a
-    stream of calls overlaps one call's host ranking with the next call's search.
+    stream of calls overlaps one call's host ranking with the next call's search.  Without deferral, a large search
+    over a large table runs as ``sub_blocks`` launches over consecutive slices of the active list (default
+    :func:`_tie_sub_blocks`), and each slice's tied rows are ranked on the host while the next slice searches.
     """
     if sig.dim() != 1 or sig.dtype != torch.float32 or not sig.is_cuda:
         raise ValueError("compress_device expects a 1-D float32 device tensor")
@@ -264,20 +267,25 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
         call("fwav_prune", rsh.data_ptr(), m, lo, rs, float(F32(energy_thresh * 0.75)), int(bool(fast_mode)),
              emb.data_ptr(), nd, k, zc.data_ptr(), cand.data_ptr(), active.data_ptr(), n_active.data_ptr(), st)
         _mark(events, "prune")
-        _mark(events, "sim_topk")
-        wk = size_call("fwav_sim_topk_workspace_size", m, nd, k) if (emb16 is not None or k > 64) else 0
-        wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
-        ties = (torch.empty(size_call("fwav_tie_list_size", m), dtype=torch.int32, device=dev)
-                if tie_order != "index" else None)
-        call("fwav_sim_topk", emb.data_ptr(), _p(emb16), nd, active.data_ptr(), n_active.data_ptr(), m, lo, k, threads,
-             cand.data_ptr(), _p(ties), wsk.data_ptr(), wk, st)
-        _mark(events, "sim_topk")
-        _mark(events, "affine")
         sc = float(abs(F32(s_clip)))
-        call("fwav_affine", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, sc, idx.data_ptr(),
-             s.data_ptr(), o.data_ptr(), sym.data_ptr(), err.data_ptr(), st)
-        _mark(events, "affine")
-        if ties is not None:
+        nsub = 1
+        if tie_order != "index" and not defer_ties:
+            nsub = int(sub_blocks) if sub_blocks is not None else _tie_sub_blocks(m, nd)
+            nsub = max(1, min(nsub, m))
+        if nsub == 1:
+            _mark(events, "sim_topk")
+            wk = size_call("fwav_sim_topk_workspace_size", m, nd, k) if (emb16 is not None or k > 64) else 0
+            wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
+            ties = (torch.empty(size_call("fwav_tie_list_size", m), dtype=torch.int32, device=dev)
+                    if tie_order != "index" else None)
+            call("fwav_sim_topk", emb.data_ptr(), _p(emb16), nd, active.data_ptr(), n_active.data_ptr(), m, lo, k,
+                 threads, cand.data_ptr(), _p(ties), wsk.data_ptr(), wk, st)
+            _mark(events, "sim_topk")
+            _mark(events, "affine")
+            call("fwav_affine", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, sc, idx.data_ptr(),
+                 s.data_ptr(), o.data_ptr(), sym.data_ptr(), err.data_ptr(), st)
+            _mark(events, "affine")
+        if nsub == 1 and ties is not None:
             # exactly tied scores whose order can change a match: numpy's own ranking for those rows (fwav.ties)
             _mark(events, "ties")
             resolve = torch.empty(m + 1, dtype=torch.int32, device=dev)
@@ -297,12 +305,78 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
             else:
                 finish(st)
             _mark(events, "ties")
+        elif nsub > 1:
+            ties = _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb16, active, n_active,
+                                      rsh, pool, cand, (idx, s, o, sym, err), res, events, st)
     res.pool, res.idx, res.s, res.o, res.sym, res.err, res.n_active = pool, idx, s, o, sym, err, n_active
     if keep_intermediates:
         res.ranges, res.emb, res.cand, res.active = ranges, emb, cand, active
         if m > 0 and ties is not None:
             res.ties = ties
     return res
+
+
+#: query sub-blocks of a search whose tied rows are ranked while the next sub-block searches: only where numpy's
+#: ranking of a row is expensive (tables of ≥ 4 Mi domains: a cfg3 row 13 ms, a cfg4 row ≈ 50 ms on the host) and
+#: every sub-block still fills the chip for a few rounds (≥ 400,000 queries; a slice launch costs ≈ 26 ms more at
+#: cfg3, 60 ms at cfg4: profiles/r03/sub_blocks_cfg3.log, sub_blocks_cfg4_eighth.log)
+SUB_BLOCK_MIN_DOMAINS = 1 << 22
+SUB_BLOCK_QUERIES = 400_000
+
+
+def _tie_sub_blocks(m: int, nd: int) -> int:
+    if nd < SUB_BLOCK_MIN_DOMAINS:
+        return 1
+    return max(1, min(8, m // SUB_BLOCK_QUERIES))
+
+
+def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb16, active, n_active, rsh, pool, cand,
+                       outs, res, events, st):
+    """The search as ``nsub`` launches over consecutive slices of the active list.  After each slice's search and tie
+    check the host reads its tie counts (one synchronisation), queues the exact score rows of its tied rows and hands
+    their copies and numpy's ranking to the driver thread (fwav.ties.rank_rows_async); then the next slice searches.
+    The affine solve runs once over the shard after the last slice, then the ranked rows are applied."""
+    dev = rsh.device
+    bounds = [(m * j // nsub, m * (j + 1) // nsub) for j in range(nsub)]
+    wk = max(size_call("fwav_sim_topk_workspace_size", b - a, nd, k) for a, b in bounds) \
+        if (emb16 is not None or k > 64) else 0
+    wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
+    pend = []
+    n_ties = n_res = 0
+    _mark(events, "sim_topk")
+    for j0, j1 in bounds:
+        mq = j1 - j0
+        na = torch.clamp(n_active - j0, 0, mq).to(torch.int32)
+        ties = torch.empty(size_call("fwav_tie_list_size", mq), dtype=torch.int32, device=dev)
+        call("fwav_sim_topk", emb.data_ptr(), _p(emb16), nd, active[j0:].data_ptr(), na.data_ptr(), mq, lo, k, threads,
+             cand.data_ptr(), ties.data_ptr(), wsk.data_ptr(), wk, st)
+        resolve = torch.empty(mq + 1, dtype=torch.int32, device=dev)
+        call("fwav_tie_check", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, emb.data_ptr(), lo,
+             threads, ties.data_ptr(), mq, int(tie_order == "numpy_sets"), resolve.data_ptr(), st)
+        counts = torch.stack([ties[0], resolve[0]]).cpu()
+        if _ties._TRACE:
+            import time
+            print(f"fwav.engine {time.perf_counter():.4f}: slice {j0}..{j1} searched, {int(counts[1])} tied rows",
+                  flush=True)
+        n_ties += int(counts[0])
+        nr_j = int(counts[1])
+        n_res += nr_j
+        if nr_j:
+            rows = resolve[1:1 + nr_j]
+            pend.append((rows, _ties.rank_rows_async(rows, emb=emb, n_domains=nd, q_offset=lo, k=k, threads=threads,
+                                                     stream=st)))
+    _mark(events, "sim_topk")
+    _mark(events, "affine")
+    call("fwav_affine", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, sc, *[t.data_ptr() for t in outs],
+         st)
+    _mark(events, "affine")
+    _mark(events, "ties")
+    for rows, fut in pend:
+        _ties.apply_rows(rows, fut.result(), ranges=rsh, range_size=rs, pool=pool, n_domains=nd, k=k, s_clip=sc,
+                         cand=cand, outs=outs, stream=st)
+    _mark(events, "ties")
+    res.n_ties, res.n_resolved = n_ties, n_res
+    return None
 
 
 def decompress_device(idx: torch.Tensor, *args, **kwargs):

@@ -19,6 +19,7 @@ the device; numpy only orders equal keys, exactly as it does in the reference.
 from __future__ import annotations
 
 import os
+import threading
 import time
 
 import numpy as np
@@ -30,8 +31,13 @@ from ._lib import call
 DEVICE_ROW_BUDGET = 2 << 30
 #: page-locked host bytes of score rows in flight (one slot per row being ranked)
 HOST_ROW_BUDGET = 4 << 30
+MAX_SLOTS = 64
+#: device bytes of score rows queued at once between the query sub-blocks of a search (fwav.engine): all of a
+#: sub-block's rows in one launch, so that none waits behind the next sub-block's search
+PIPE_ROW_BUDGET = 16 << 30
 
 _BLAS_THREADS = None
+_TRACE = bool(os.environ.get("FWAV_TIES_TRACE"))
 
 
 def blas_threads() -> int:
@@ -72,18 +78,26 @@ def numpy_topk_row(scores: np.ndarray, k: int) -> np.ndarray:
 
 _POOL = None
 _SLOTS: list = []
+_SLOT_BUSY: list = []  # per staging slot: the future ranking the row it holds (None when free)
+_SLOT_LOCK = threading.Lock()  # one staging loop at a time owns the slot ring
+_SLOT_NEXT = 0
 _DRIVER = None
 _SIDE: dict = {}
+_COPY: dict = {}
+
+
+def _driver():
+    global _DRIVER
+    if _DRIVER is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _DRIVER = ThreadPoolExecutor(1, thread_name_prefix="fwav-ties-driver")
+    return _DRIVER
 
 
 def defer(finish, device: torch.device):
     """Run ``finish(stream)`` — the host half of a tie resolution — on the background driver thread, on a side stream
     that first waits for everything queued so far on ``device``'s current stream.  Returns its Future.  One driver
-    thread: resolutions run in call order and share the staging buffers."""
-    global _DRIVER
-    if _DRIVER is None:
-        from concurrent.futures import ThreadPoolExecutor
-        _DRIVER = ThreadPoolExecutor(1, thread_name_prefix="fwav-ties-driver")
+    thread: resolutions run in call order."""
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(device))
     key = str(device)
@@ -99,7 +113,7 @@ def defer(finish, device: torch.device):
             finish(side.cuda_stream)
             side.synchronize()
 
-    return _DRIVER.submit(job)
+    return _driver().submit(job)
 
 
 def _pool():
@@ -114,7 +128,7 @@ def _pool():
 
 
 def _slot(i: int, numel: int) -> torch.Tensor:
-    """Reusable page-locked staging row i (float32), grown on demand."""
+    """Reusable page-locked staging row i (float32), grown on demand (caller holds _SLOT_LOCK, slot i free)."""
     while len(_SLOTS) <= i:
         _SLOTS.append(None)
     t = _SLOTS[i]
@@ -122,6 +136,116 @@ def _slot(i: int, numel: int) -> torch.Tensor:
         t = torch.empty(numel, dtype=torch.float32, pin_memory=True)
         _SLOTS[i] = t
     return t[:numel]
+
+
+def score_row_launches(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, threads: int,
+                       stream: int, budget: int = DEVICE_ROW_BUDGET):
+    """Yield (first row, device f32[m·nd] scores, event) per fwav_score_rows launch of at most ``budget`` bytes,
+    each launch queued on the current stream (``stream``) when the generator reaches it."""
+    nd = int(n_domains)
+    n = rows.numel()
+    per = max(1, min(n, budget // (4 * nd)))
+    for b0 in range(0, n, per):
+        rb = rows[b0:b0 + per].contiguous()
+        m = rb.numel()
+        S = torch.empty(m * nd, dtype=torch.float32, device=rows.device)
+        call("fwav_score_rows", emb.data_ptr(), nd, rb.data_ptr(), m, int(q_offset), int(threads), S.data_ptr(),
+             stream)
+        ev = torch.cuda.Event()
+        ev.record()
+        yield b0, S, ev
+
+
+def rank_rows(launches, n: int, n_domains: int, k: int, copy_stream=None) -> list:
+    """Copy the score rows of ``launches`` (score_row_launches) to the ring of page-locked slots (HOST_ROW_BUDGET)
+    in runs of at most one slot per row, one synchronisation per run, and hand each landed row to numpy's ranking on
+    the host pool.  Returns the n futures (candidate rows, int32[k]).  ``copy_stream``: the copies' stream (it waits
+    for each launch's event), else the current stream."""
+    nd = int(n_domains)
+    nslots = max(2, min(MAX_SLOTS, HOST_ROW_BUDGET // (4 * nd)))  # the ring (slots are allocated on first use)
+    ex = _pool()
+    futs = [None] * n
+    done = torch.cuda.Event()
+    global _SLOT_NEXT
+    with _SLOT_LOCK:
+        while len(_SLOT_BUSY) < nslots:
+            _SLOT_BUSY.append(None)
+        base = _SLOT_NEXT  # consecutive calls take the ring's next slots, not the ones the last call is still ranking
+        for b0, S, ev in launches:
+            m = S.numel() // nd
+            if copy_stream is not None:
+                copy_stream.wait_event(ev)
+            for r0 in range(0, m, nslots):
+                hs = []
+                for i in range(b0 + r0, b0 + min(m, r0 + nslots)):
+                    sl = (base + i) % nslots
+                    if _SLOT_BUSY[sl] is not None:  # its previous row is still being ranked
+                        _SLOT_BUSY[sl].result()
+                        _SLOT_BUSY[sl] = None
+                    h = _slot(sl, nd)
+                    src = S[(i - b0) * nd:(i - b0 + 1) * nd]
+                    if copy_stream is not None:
+                        with torch.cuda.stream(copy_stream):
+                            h.copy_(src, non_blocking=True)
+                    else:
+                        h.copy_(src, non_blocking=True)
+                    hs.append((i, sl, h))
+                if copy_stream is not None:
+                    done.record(copy_stream)
+                else:
+                    done.record()
+                done.synchronize()
+                if _TRACE:
+                    print(f"fwav.ties {time.perf_counter():.4f}: rows {hs[0][0]}..{hs[-1][0]} of {n} on the host",
+                          flush=True)
+                for i, sl, h in hs:
+                    futs[i] = _SLOT_BUSY[sl] = ex.submit(numpy_topk_row, h.numpy(), k)
+            del S
+        _SLOT_NEXT = (base + n) % nslots
+    return futs
+
+
+def rank_rows_async(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, k: int, threads: int,
+                    stream: int):
+    """Queue every exact score row of ``rows`` now (one launch per PIPE_ROW_BUDGET), and copy + rank them on the
+    driver thread (copies on a copy stream that waits for the launches).  Returns a Future of the n row futures.
+    Used between the query sub-blocks of one search (fwav.engine), so that the next sub-block's search does not
+    delay the score rows: only their copies and numpy's ranking overlap it."""
+    n = rows.numel()
+    launches = list(score_row_launches(rows, emb=emb, n_domains=n_domains, q_offset=q_offset, threads=threads,
+                                       stream=stream, budget=PIPE_ROW_BUDGET))
+    dev = rows.device
+    key = str(dev)
+    if key not in _COPY:
+        _COPY[key] = torch.cuda.Stream(dev)
+    cs = _COPY[key]
+
+    def job():
+        def it():  # each launch's scores are released once its rows are on the host
+            while launches:
+                yield launches.pop(0)
+        with torch.cuda.device(dev):
+            return rank_rows(it(), n, n_domains, k, copy_stream=cs)
+
+    return _driver().submit(job)
+
+
+def apply_rows(rows: torch.Tensor, futs: list, *, ranges: torch.Tensor, range_size: int, pool: torch.Tensor,
+               n_domains: int, k: int, s_clip: float, cand: torch.Tensor, outs: tuple, stream: int) -> None:
+    """Write numpy's candidate rows (the futures of rank_rows) into ``cand`` and re-run the affine solve for those
+    rows into ``outs`` = (idx, s, o, sym, err), on the current stream (``stream``)."""
+    dev = rows.device
+    n = rows.numel()
+    newc = torch.from_numpy(np.stack([f.result() for f in futs])).to(dev)
+    ridx = rows.long()
+    cand.view(-1, k)[ridx] = newc
+    rs = int(range_size)
+    rsub = ranges.view(-1, rs)[ridx].contiguous()
+    tmp = [torch.empty(n, dtype=t.dtype, device=dev) for t in outs]
+    call("fwav_affine", rsub.data_ptr(), n, rs, newc.data_ptr(), k, pool.data_ptr(), int(n_domains), float(s_clip),
+         *[t.data_ptr() for t in tmp], stream)
+    for t, u in zip(outs, tmp):
+        t[ridx] = u
 
 
 def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, k: int, threads: int,
@@ -133,55 +257,18 @@ def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_off
     candidate rows written back to ``cand`` and the affine solve re-run for those rows into ``outs`` =
     (idx, s, o, sym, err).  (cfg4-sized rows, 86.4 M scores: 22 rows 3.5 → 1.1 s against one 256 MB
     double buffer.)"""
-    dev = rows.device
     n = rows.numel()
     if n == 0:
         return
     trace = os.environ.get("FWAV_TIES_TRACE")
     t0 = time.perf_counter()
-    tw = 0.0
-    nd = int(n_domains)
-    per = max(1, min(n, DEVICE_ROW_BUDGET // (4 * nd)))     # rows per fwav_score_rows launch
-    nslots = max(2, min(n, HOST_ROW_BUDGET // (4 * nd)))   # rows staged on the host at once
-    cv = cand.view(-1, k)
-    ex = _pool()
-    futs = [None] * n
-    slot_busy = [None] * nslots  # the future ranking each slot's row
-    S = torch.empty(per * nd, dtype=torch.float32, device=dev)
-    ev = torch.cuda.Event()
-    for b0 in range(0, n, per):
-        rb = rows[b0:b0 + per].contiguous()
-        m = rb.numel()
-        call("fwav_score_rows", emb.data_ptr(), nd, rb.data_ptr(), m, int(q_offset), int(threads), S.data_ptr(),
-             stream)
-        # copy the launch's rows to free staging slots in runs of at most nslots, one synchronisation per run
-        for r0 in range(0, m, nslots):
-            run = range(b0 + r0, b0 + min(m, r0 + nslots))
-            hs = []
-            for i in run:
-                sl = i % nslots
-                if slot_busy[sl] is not None:  # its previous row is still being ranked
-                    slot_busy[sl].result()
-                h = _slot(sl, nd)
-                h.copy_(S[(i - b0) * nd:(i - b0 + 1) * nd], non_blocking=True)
-                hs.append((i, sl, h))
-            ev.record()
-            tw0 = time.perf_counter()
-            ev.synchronize()
-            tw += time.perf_counter() - tw0
-            for i, sl, h in hs:
-                futs[i] = slot_busy[sl] = ex.submit(numpy_topk_row, h.numpy(), k)
+    futs = rank_rows(score_row_launches(rows, emb=emb, n_domains=n_domains, q_offset=q_offset, threads=threads,
+                                        stream=stream), n, n_domains, k)
     t1 = time.perf_counter()
-    newc = torch.from_numpy(np.stack([f.result() for f in futs])).to(dev)
+    for f in futs:
+        f.result()
     if trace:
-        print(f"fwav.ties: {n} rows x {nd}: {(time.perf_counter() - t0) * 1e3:.1f} ms (device score rows + copies "
-              f"waited {tw * 1e3:.1f} ms, numpy tail {(time.perf_counter() - t1) * 1e3:.1f} ms)", flush=True)
-    ridx = rows.long()
-    cv[ridx] = newc
-    rs = int(range_size)
-    rsub = ranges.view(-1, rs)[ridx].contiguous()
-    tmp = [torch.empty(n, dtype=t.dtype, device=dev) for t in outs]
-    call("fwav_affine", rsub.data_ptr(), n, rs, newc.data_ptr(), k, pool.data_ptr(), nd, float(s_clip),
-         *[t.data_ptr() for t in tmp], stream)
-    for t, u in zip(outs, tmp):
-        t[ridx] = u
+        print(f"fwav.ties: {n} rows x {n_domains}: {(time.perf_counter() - t0) * 1e3:.1f} ms (device score rows + "
+              f"copies {(t1 - t0) * 1e3:.1f} ms, numpy tail {(time.perf_counter() - t1) * 1e3:.1f} ms)", flush=True)
+    apply_rows(rows, futs, ranges=ranges, range_size=range_size, pool=pool, n_domains=n_domains, k=k, s_clip=s_clip,
+               cand=cand, outs=outs, stream=stream)

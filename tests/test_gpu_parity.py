@@ -137,10 +137,6 @@ def test_reference_e2e_tone(tmp_path):
     assert snr > 4.0
     g = load("tone")
     assert len(matches) == len(g["m_idx_32"])
-    # the .fwav bytes equal the reference's wherever the tuples agree (fractal.py:1278-1322: header, SHA-256 of the
-    # body, pool, 17-byte match records): header and pool always; every match record but those of the tone's
-    # byte-identical-tile ranges (equal fits, rule 4), whose (idx, sym) follow a different tie order — and with
-    # them the digest
     # the .fwav written here is the reference's file byte for byte (fractal.py:1278-1322: header, SHA-256 of the
     # body, pool, 17-byte match records) — the tone's byte-identical tiles included, whose matches follow numpy's
     # order among exactly tied scores
@@ -471,3 +467,25 @@ def test_deferred_tie_resolution_equals_synchronous():
         assert (r.n_ties, r.n_resolved) == (ref.n_ties, ref.n_resolved)
         for nm in ("cand", "idx", "s", "o", "sym", "err"):
             assert bit_equal(getattr(r, nm).cpu().numpy(), getattr(ref, nm).cpu().numpy()), nm
+
+
+@pytest.mark.parametrize("nsub", [2, 5])
+def test_sub_block_search_equals_single_launch(nsub):
+    """sub_blocks=n (the search as n launches over slices of the active list, each slice's tied rows ranked on the
+    host while the next slice searches — the default for large searches over ≥ 4 Mi-domain tables): every output,
+    the tie counts and the candidate rows equal the single launch's (tone, K = 32: rows that numpy re-ranks; speech:
+    pruned ranges, so slices hold uneven parts of the active list)."""
+    for name, k in (("tone", 32), ("speech4096", 64)):
+        g = load(name)
+        p = g["p"]
+        sig = td(g["signal"])
+        ref = engine.compress_device(sig, p["tile"], k, energy_thresh=p["thr"], keep_intermediates=True,
+                                     sub_blocks=1)
+        got = engine.compress_device(sig, p["tile"], k, energy_thresh=p["thr"], keep_intermediates=True,
+                                     sub_blocks=nsub)
+        torch.cuda.synchronize()
+        if name == "tone":
+            assert ref.n_resolved > 0
+        assert (got.n_ties, got.n_resolved) == (ref.n_ties, ref.n_resolved), name
+        for nm in ("cand", "idx", "s", "o", "sym", "err"):
+            assert bit_equal(getattr(got, nm).cpu().numpy(), getattr(ref, nm).cpu().numpy()), (name, nm)
