@@ -321,6 +321,7 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
 #: every sub-block still fills the chip for a few rounds (≥ 400,000 queries; a slice launch costs ≈ 26 ms more at
 #: cfg3, 60 ms at cfg4: profiles/r03/sub_blocks_cfg3.log, sub_blocks_cfg4_eighth.log)
 SUB_BLOCK_MIN_DOMAINS = 1 << 22
+TIE_REC = 9  # int32 per tie record (kTieRec, fwav_common.h)
 SUB_BLOCK_QUERIES = 400_000
 
 
@@ -335,13 +336,15 @@ def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb1
     """The search as ``nsub`` launches over consecutive slices of the active list.  After each slice's search and tie
     check the host reads its tie counts (one synchronisation), queues the exact score rows of its tied rows and hands
     their copies and numpy's ranking to the driver thread (fwav.ties.rank_rows_async); then the next slice searches.
-    The affine solve runs once over the shard after the last slice, then the ranked rows are applied."""
+    The affine solve runs once over the shard after the last slice, then the ranked rows are applied.  Returns the
+    slices' tie records as one list."""
     dev = rsh.device
     bounds = [(m * j // nsub, m * (j + 1) // nsub) for j in range(nsub)]
     wk = max(size_call("fwav_sim_topk_workspace_size", b - a, nd, k) for a, b in bounds) \
         if (emb16 is not None or k > 64) else 0
     wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
     pend = []
+    lists = []  # each slice's tie records
     n_ties = n_res = 0
     _mark(events, "sim_topk")
     for j0, j1 in bounds:
@@ -359,6 +362,7 @@ def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb1
             print(f"fwav.engine {time.perf_counter():.4f}: slice {j0}..{j1} searched, {int(counts[1])} tied rows",
                   flush=True)
         n_ties += int(counts[0])
+        lists.append(ties[1:1 + TIE_REC * int(counts[0])])
         nr_j = int(counts[1])
         n_res += nr_j
         if nr_j:
@@ -376,7 +380,8 @@ def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb1
                          cand=cand, outs=outs, stream=st)
     _mark(events, "ties")
     res.n_ties, res.n_resolved = n_ties, n_res
-    return None
+    # one tie list in fwav_sim_topk's layout (count, then the records of every slice)
+    return torch.cat([torch.tensor([n_ties], dtype=torch.int32, device=dev)] + lists)
 
 
 def decompress_device(idx: torch.Tensor, *args, **kwargs):

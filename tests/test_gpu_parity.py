@@ -489,3 +489,9 @@ def test_sub_block_search_equals_single_launch(nsub):
         assert (got.n_ties, got.n_resolved) == (ref.n_ties, ref.n_resolved), name
         for nm in ("cand", "idx", "s", "o", "sym", "err"):
             assert bit_equal(getattr(got, nm).cpu().numpy(), getattr(ref, nm).cpu().numpy()), (name, nm)
+        # the slices' tie lists, merged, name the single launch's queries and boundary flags (records land in
+        # completion order: compare sorted)
+        def recs(r):
+            t = r.ties.cpu().numpy()
+            return np.sort(t[1:1 + 9 * int(t[0])].reshape(-1, 9)[:, 0])
+        assert np.array_equal(recs(got), recs(ref)), name
