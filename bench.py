@@ -168,7 +168,10 @@ def main():
     backend = os.environ.get("FWAV_BENCH_BACKEND", "nccl")
     dev_index = local % torch.cuda.device_count() if os.environ.get("FWAV_BENCH_SHARE_GPU") else local
     torch.cuda.set_device(dev_index)
-    if world > 1:
+    # FWAV_BENCH_FORCE_DIST=1 runs the multi-rank path at world size 1 (its collectives included) — a check of the
+    # RCCL calls on a one-GPU box; the value is then the sharded path's, not the N = 1 line
+    sharded = world > 1 or bool(os.environ.get("FWAV_BENCH_FORCE_DIST"))
+    if sharded:
         import torch.distributed as dist  # noqa: F811
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
@@ -187,7 +190,7 @@ def main():
     torch.cuda.synchronize()
 
     phase = {}
-    if world == 1:
+    if not sharded:
         def step(ev=None):
             # the host half of numpy-order tie resolution (a few rows per step) overlaps the next step's search;
             # every step's outputs are final (wait()) before the timed region closes
@@ -222,13 +225,13 @@ def main():
 
         step.inflight = []
 
-    if world == 1:
+    if not sharded:
         step.pending = []
 
     def drain():
         for r in getattr(step, "pending", []):
             r.wait()
-        if world == 1:
+        if not sharded:
             step.pending = []
         while getattr(step, "inflight", None):
             step.out = fdist.compress_sharded_finish(step.inflight.pop(0))
@@ -281,7 +284,7 @@ def main():
     t_topk = stage_ms["sim_topk"] * 1e-3
     flops = 2.0 * n_active * nd * 16
     achieved_tf = flops / t_topk / 1e12
-    traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
+    traffic, traffic_src = pmc_traffic(args.config) if not sharded else (None, None)
     line = {
         "metric": "ranges matched/sec at tile_size=2048, top-K=64",
         "value": value, "unit": "ranges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -291,7 +294,7 @@ def main():
                                f"{WORKLOAD_TEXT.get(args.config, '').split(' ', 4)[-1]}, tile_size={tile}, "
                                f"top_k={K}, n_ranges={nr}, n_domains={nd}",
                    "tile_size": tile, "top_k": K, "n_ranges": nr, "n_domains": nd,
-                   "parallelism": "single GPU" if world == 1 else f"ranges sharded x{world} (RCCL broadcast + "
+                   "parallelism": "single GPU" if not sharded else f"ranges sharded x{world} (RCCL broadcast + "
                                                                   f"gather)"},
         "roofline": {"kernel": f"{TOPK_KERNEL} (fp16 MFMA similarity GEMM pre-filter + streaming exact top-K)",
                      "bound": "mfma", "achieved": achieved_tf, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s",
@@ -303,7 +306,7 @@ def main():
     }
     if per_rank is not None:
         line["per_rank"] = per_rank
-    extras = world == 1 and not args.no_extras
+    extras = not sharded and not args.no_extras
     if extras:
         # Host-boundary rate (not `value`): numpy signal in host memory → matches (SoA) back in host memory.
         def e2e_step():
