@@ -55,6 +55,16 @@ def _broadcast_(t: torch.Tensor, group, device: torch.device) -> torch.Tensor:
     return t
 
 
+_SIDE: dict = {}
+
+
+def _side_stream(device: torch.device):
+    key = str(device)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device)
+    return _SIDE[key]
+
+
 def _sync(device: torch.device) -> None:
     if device.type == "cuda":
         torch.cuda.synchronize(device)
@@ -130,8 +140,9 @@ def compress_sharded_device(sig: Optional[torch.Tensor], tile_size: int, top_k: 
                             group=None, device: Optional[torch.device] = None, compute: Optional[Callable] = None,
                             timings: Optional[dict] = None, n: Optional[int] = None):
     """The sharded compress on device tensors.  ``sig`` (1-D f32, on ``device``) is needed on rank 0 only.
-    Returns on rank 0 a dict of full-length device tensors idx/s/o/sym/err, the pool, the blocks and geometry;
-    None on the other ranks.  ``n`` (the signal length, if every rank knows it) saves broadcasting it.
+    Returns on rank 0 a dict of full-length device tensors idx/s/o/sym/err, the pool, the blocks and geometry, and
+    ``is_silent()`` (the reference's silent-input test, one device read); None on the other ranks (``empty=True``
+    without arrays for empty / short input).  ``n`` (the signal length, if every rank knows it) saves broadcasting it.
     ``timings`` (if given) receives per-phase host seconds (broadcast / compute / gather), each phase then closed by
     a device synchronisation (without it the phases run back to back, with no synchronisation of their own).
     Equal to ``compress_sharded_finish(compress_sharded_start(...))``."""
@@ -141,12 +152,15 @@ def compress_sharded_device(sig: Optional[torch.Tensor], tile_size: int, top_k: 
 
 def compress_sharded_start(sig: Optional[torch.Tensor], tile_size: int, top_k: int, energy_thresh: float = 1e-4,
                            group=None, device: Optional[torch.device] = None, compute: Optional[Callable] = None,
-                           timings: Optional[dict] = None, n: Optional[int] = None) -> dict:
+                           timings: Optional[dict] = None, n: Optional[int] = None,
+                           signal_ready: bool = False) -> dict:
     """First half of :func:`compress_sharded_device`: the signal broadcast and this rank's search + solve, queued.
     ``compute`` may return a ``wait`` callable (a deferred tie resolution, engine.compress_device(defer_ties=True));
     :func:`compress_sharded_finish` calls it before the gather.  A stream of calls can keep a few started calls in
     flight and finish them in order, so that one call's host tie ranking overlaps the next calls' searches (bench.py);
-    every rank must start and finish the same calls in the same order (the collectives pair up by order)."""
+    every rank must start and finish the same calls in the same order (the collectives pair up by order).
+    ``signal_ready=True`` (rank 0): ``sig`` is complete on every stream, so the broadcast need not wait for the work
+    already queued on the current stream."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     if device is None:
@@ -167,16 +181,36 @@ def compress_sharded_start(sig: Optional[torch.Tensor], tile_size: int, top_k: i
             n_t[0] = int(sig.numel())
         _broadcast_(n_t, group, device)
         n = int(n_t.item())
-    if rank != 0:
-        sig = torch.empty(n, dtype=torch.float32, device=device)
-    _broadcast_(sig, group, device)  # the one data-path collective before the search
-    t1 = mark()
-
     rs, step = geometry(tile_size)
     blocks_box: list = []
+    pre = None
+    if device.type == "cuda" and n > 0:
+        # Broadcast, ranges and shard bounds on a side stream: the bounds' host synchronisation then waits for these
+        # few kernels only, not for the calls still searching on the main stream (a stream of calls keeps the
+        # device busy).  The search reads the ranges again on the main stream (a few hundred µs, bit-identical).
+        main = torch.cuda.current_stream(device)
+        side = _side_stream(device)
+        if rank == 0 and not signal_ready:
+            side.wait_stream(main)  # the signal may still be in flight on the main stream
+        with torch.cuda.stream(side):
+            if rank != 0:
+                sig = torch.empty(n, dtype=torch.float32, device=device)
+            _broadcast_(sig, group, device)  # the one data-path collective before the search
+            if world > 1:
+                from .engine import ranges_device
+                rg, nr_, rs_ = ranges_device(sig, tile_size, energy_thresh)
+                pre = prune_balanced_bounds(rg, nr_, rs_, energy_thresh, world)
+        main.wait_stream(side)
+        sig.record_stream(main)
+    else:
+        if rank != 0:
+            sig = torch.empty(n, dtype=torch.float32, device=device)
+        _broadcast_(sig, group, device)  # the one data-path collective before the search
+    t1 = mark()
 
     def shard(ranges, n_ranges, range_size):
-        blocks_box[:] = prune_balanced_bounds(ranges, n_ranges, range_size, energy_thresh, world)
+        blocks_box[:] = pre if pre is not None else prune_balanced_bounds(ranges, n_ranges, range_size, energy_thresh,
+                                                                          world)
         return blocks_box[rank]
 
     res = compute(sig, tile_size, top_k, energy_thresh, shard)
@@ -208,9 +242,11 @@ def compress_sharded_finish(h: dict):
     if rank != 0:
         return None
     out = _unpack(torch.stack(glist), blocks)
+    # the silent-input test reads a device value: left to the caller (compress_sharded), so that a stream of calls
+    # does not synchronise here with the calls still in flight
     silent = res.get("silent")
-    out.update(empty=bool(silent()) if callable(silent) else False, n_ranges=nr, range_size=rs, domain_step=step,
-               original_len=n, pool=res["pool"], blocks=blocks)
+    out.update(is_silent=silent if callable(silent) else (lambda: False), n_ranges=nr, range_size=rs,
+               domain_step=step, original_len=n, pool=res["pool"], blocks=blocks)
     return out
 
 
@@ -234,6 +270,7 @@ def compress_sharded(signal: Optional[np.ndarray], tile_size: int, top_k: int, e
     if out.get("empty") and "idx" not in out:
         return out
     host = {f: out[f].cpu().numpy() for f in FIELDS}
+    host["empty"] = bool(out.pop("is_silent")())
     pool = out["pool"]
     pool = pool.cpu().numpy() if isinstance(pool, torch.Tensor) else np.asarray(pool)
     host.update({k: v for k, v in out.items() if k not in FIELDS and k != "pool"})

@@ -157,6 +157,32 @@ def _empty(n, rs, tile, step, thr, k) -> DeviceCompressed:
     return DeviceCompressed(0, rs, tile, step, thr, n, 0, k, (0, 0), empty=True)
 
 
+def _voiced_ranges(sig, n, rs, frame, thr32, lo32, st) -> torch.Tensor:
+    """fwav_voiced_ranges on the stream ``st``: the voiced-masked, reflect-padded ranges f32[nr·rs]."""
+    nr = -(-n // rs)
+    ws_n = size_call("fwav_voiced_workspace_size", n, frame)
+    ws = torch.empty(ws_n, dtype=torch.uint8, device=sig.device)
+    ranges = torch.empty(nr * rs, dtype=torch.float32, device=sig.device)
+    call("fwav_voiced_ranges", sig.data_ptr(), n, rs, frame, 5, float(thr32), float(lo32), ranges.data_ptr(), nr,
+         None, ws.data_ptr(), ws_n, st)
+    return ranges
+
+
+def ranges_device(sig: torch.Tensor, tile_size: int, energy_thresh: float = 1e-4) -> tuple[torch.Tensor, int, int]:
+    """The ranges alone (voiced detection + range formation, fractal.py:880-909, 1074-1112) on the current stream of
+    ``sig``'s device: (ranges f32[nr·rs], nr, rs) — what fwav.dist needs to balance the shards before a compress."""
+    if sig.dim() != 1 or sig.dtype != torch.float32 or not sig.is_cuda:
+        raise ValueError("ranges_device expects a 1-D float32 device tensor")
+    with torch.cuda.device(sig.device):
+        sig = sig.contiguous()
+        n = sig.numel()
+        rs, _ = geometry(tile_size)
+        if n == 0:
+            raise ValueError("a cannot be empty")
+        r = _voiced_ranges(sig, n, rs, 2 * rs, F32(energy_thresh), F32(energy_thresh * 0.5), _stream(sig.device))
+        return r, -(-n // rs), rs
+
+
 def compress_device(sig: torch.Tensor, *args, **kwargs) -> DeviceCompressed:
     """Run the compress hot path on ``sig``'s device (made current for the call: the C ABI's per-device plans and
     kernel attributes are taken from the current HIP device).  See :func:`_compress_device`."""
@@ -212,12 +238,8 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
         raise ValueError("tie_order must be 'numpy' (the reference's order of exactly tied scores wherever it decides a"
                          " match), 'numpy_sets' (and wherever it decides a candidate set) or 'index'")
     threads = _ties.blas_threads() if blas_threads is None else int(blas_threads)
-    ws_n = size_call("fwav_voiced_workspace_size", n, frame)
-    ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
-    ranges = torch.empty(nr * rs, dtype=torch.float32, device=dev)
     _mark(events, "voiced_ranges")
-    call("fwav_voiced_ranges", sig.data_ptr(), n, rs, frame, 5, float(thr32), float(lo32), ranges.data_ptr(), nr,
-         None, ws.data_ptr(), ws_n, st)
+    ranges = _voiced_ranges(sig, n, rs, frame, thr32, lo32, st)
     partial = torch.empty(1, dtype=torch.float32, device=dev)
     wse = size_call("fwav_weighted_energy_workspace_size", n)
     wsen = torch.empty(wse, dtype=torch.uint8, device=dev)

@@ -198,7 +198,7 @@ def main():
             step.pending.append(r)
             return r
     else:
-        LAG = 2  # started calls in flight before the oldest is finished (its ties waited for, its matches gathered)
+        LAG = 3  # started calls in flight before the oldest is finished (its ties waited for, its matches gathered)
 
         def step(ev=None, phases=False):
             def compute(s, t, k, thr, shard):
@@ -210,7 +210,7 @@ def main():
             # device at each phase boundary) are taken on extra unpipelined steps after the timed ones
             tm = {} if phases else None
             h = fdist.compress_sharded_start(sig, tile, K, 1e-4, device=dev, compute=compute, timings=tm,
-                                             n=int(sig_h.size))
+                                             n=int(sig_h.size), signal_ready=True)
             if phases:
                 step.out = fdist.compress_sharded_finish(h)
                 for k_, v in tm.items():
