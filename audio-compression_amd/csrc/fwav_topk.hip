@@ -1630,7 +1630,7 @@ static void topk_device_slots(bool wide, int& cus, int& per_cu) {
   int& w = ws[wide][dev];
   if (c == 0) {
     const hipError_t occ =
-        wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeHL, kWideW, kWideG>,
+        wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeHL, kWideW, kWideG, 1>,
                                                             64 * kWideW, 0)
              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeS16>, 64 * k16Waves,
                                                             0);
@@ -1743,7 +1743,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, DBG_, ST_,  \
       sp, ties)
 #define FWAV_FIRST_WIDE(MODE_)                                                                                   \
-  k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG><<<pl.items(), 64 * kWideW, 0, st>>>(                    \
+  k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG, 1><<<pl.items(), 64 * kWideW, 0, st>>>(                    \
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
       sp, ties)
 #ifdef FWAV_TOPK_EXTSEED
