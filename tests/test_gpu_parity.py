@@ -475,7 +475,7 @@ def test_sub_block_search_equals_single_launch(nsub):
     host while the next slice searches — the default for large searches over ≥ 4 Mi-domain tables): every output,
     the tie counts and the candidate rows equal the single launch's (tone, K = 32: rows that numpy re-ranks; speech:
     pruned ranges, so slices hold uneven parts of the active list)."""
-    for name, k in (("tone", 32), ("speech4096", 64)):
+    for name, k in (("tone", 32), ("speech4096", 64), ("speech4096", 100)):  # K = 100: the large-K kernels
         g = load(name)
         p = g["p"]
         sig = td(g["signal"])
