@@ -353,6 +353,15 @@ def _tie_sub_blocks(m: int, nd: int) -> int:
     return max(1, min(8, m // SUB_BLOCK_QUERIES))
 
 
+def _slice_bounds(m: int, nsub: int) -> list[tuple[int, int]]:
+    """Consecutive slices [a, b) of m active-list positions, the last one half-size: its tied rows are the only ones
+    ranked after the search has ended."""
+    nsub = max(1, min(int(nsub), m))
+    wts = [2] * (nsub - 1) + [1]
+    cuts = [m * sum(wts[:j]) // sum(wts) for j in range(nsub + 1)]
+    return [(cuts[j], cuts[j + 1]) for j in range(nsub) if cuts[j + 1] > cuts[j]]
+
+
 def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb16, active, n_active, rsh, pool, cand,
                        outs, res, events, st):
     """The search as ``nsub`` launches over consecutive slices of the active list.  After each slice's search and tie
@@ -361,7 +370,7 @@ def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb1
     The affine solve runs once over the shard after the last slice, then the ranked rows are applied.  Returns the
     slices' tie records as one list."""
     dev = rsh.device
-    bounds = [(m * j // nsub, m * (j + 1) // nsub) for j in range(nsub)]
+    bounds = _slice_bounds(m, nsub)
     wk = max(size_call("fwav_sim_topk_workspace_size", b - a, nd, k) for a, b in bounds) \
         if (emb16 is not None or k > 64) else 0
     wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)

@@ -140,3 +140,21 @@ def test_product_path_fails_loudly_without_device():
     from fwav._lib import FwavError
     with pytest.raises(FwavError):
         api.compress_audio(np.zeros(5000, np.float32), 44100, 4, tile_size=1024)
+
+
+def test_sub_block_slices():
+    """fwav.engine's sliced search (large tables): slices cover the active list exactly once, in order, the last one
+    about half the others; the slice count follows the table size and the query count."""
+    from fwav import engine
+    for m, n in ((2_700_000, 8), (1_653_750, 4), (10, 3), (5, 5), (3, 7), (1, 1)):
+        b = engine._slice_bounds(m, n)
+        assert b[0][0] == 0 and b[-1][1] == m and all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+        assert all(hi > lo for lo, hi in b)
+        if m >= 100 * n and n > 1:
+            sizes = [hi - lo for lo, hi in b]
+            assert abs(sizes[-1] * 2 - sizes[0]) <= 2 and len(set(sizes[:-1])) <= 2
+    assert engine._tie_sub_blocks(330_750, 1_321_977) == 1        # cfg2: table below 4 Mi domains
+    assert engine._tie_sub_blocks(1_653_750, 6_613_977) == 4      # cfg3
+    assert engine._tie_sub_blocks(2_700_000, 86_398_977) == 6     # one rank's eighth of cfg4
+    assert engine._tie_sub_blocks(21_600_000, 86_398_977) == 8    # all of cfg4 on one GPU
+    assert engine._tie_sub_blocks(100_000, 86_398_977) == 1
