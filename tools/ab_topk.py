@@ -76,7 +76,8 @@ for rnd in range(int(os.environ.get("AB_ROUNDS", 4))):
         assert rc == 0, name
         if rnd > 0:
             times[name].append(e0.elapsed_time(e1))
-        outs[name] = cand[:nq * 64] if cfg in ("cfg2", "cfg4") else cand  # rows past nq are never written
+        # only the searched rows are written (rows past nq, or the pruned ranges' rows of the engine's active list)
+        outs[name] = cand[:nq * 64] if cfg in ("cfg2", "cfg4") else cand.view(-1, 64)[active.long()]
         if rnd == 0:  # overflowed queries of this build: the i32 count at the end of its own workspace layout
             own = L.fwav_sim_topk_workspace_size(nq, nd, 64)
             o = own - 4 - 4 * max(nq, 1)  # ovf list, count, then u32 seeds[q]

@@ -53,4 +53,4 @@ for rep in range(2):
     print(f"rep {rep}: {e0.elapsed_time(e1):.2f} ms (STATS build); per query set of 32: replayed chunks "
           f"{sv[0] / qsets:.0f}, firing tiles {sv[1] / qsets:.0f}; per query: appends {sv[2] / nq:.1f}, compactions "
           f"{sv[3] / nq:.2f}; shares: barrier {sv[7] / tot:.3f} streaming {sv[9] / tot:.3f} replays {sv[4] / tot:.3f} "
-          f"(appends {sv[10] / tot:.3f}) final {sv[8] / tot:.3f}", flush=True)
+          f"(appends {sv[10] / tot:.3f}, fragment waits {sv[11] / tot:.3f}) final {sv[8] / tot:.3f}", flush=True)
