@@ -450,6 +450,10 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 constexpr int kGroup = FWAV_TOPK_G;     // chunks per barrier
 constexpr int k16Waves = FWAV_TOPK_W;   // waves per workgroup
 constexpr int k16Sets = FWAV_TOPK_QS;   // query sets of 32 per wave (each LDS fragment feeds k16Sets MFMAs)
+// final passes: bands of at most 128 keys rescored and sorted as 128 (A/B builds: 0 = always C)
+#ifndef FWAV_TOPK_SMALLSORT
+#define FWAV_TOPK_SMALLSORT 1
+#endif
 #ifndef FWAV_TOPK_CAP
 #define FWAV_TOPK_CAP 256
 #endif
@@ -656,11 +660,10 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0,
 // the back) in exact f32 (sgemv16), sort, emit the top K to `out`.  Whole wave.  Every per-query buffer and
 // counter is owned by one wave, so no cross-wave fences are needed; the wave's own appended stores are drained
 // once (vmcnt(0)), then all key loads and all row loads are issued together (two memory round trips in total).
-template <int C, class SM>
-__device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
-                                          const float* __restrict__ emb, int32_t* __restrict__ out,
-                                          const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid) {
-  constexpr int E = C / 64;
+template <int C, int E, class SM>
+__device__ __forceinline__ void compact16_e(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
+                                            const float* __restrict__ emb, int32_t* __restrict__ out,
+                                            const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid) {
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int n0 = sm.cnt[ql];
@@ -721,6 +724,19 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
     const int e = j * 64 + lane;
     if (e < K) out[e] = e < n ? key_idx(v[j]) : -1;
   }
+}
+
+// A buffer of at most 128 entries (the usual case: the band kept by the last compaction plus the few appends after
+// it) is rescored two entries per lane and sorted as 128 keys; a fuller one as C.  Same outputs either way.
+template <int C, class SM>
+__device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
+                                          const float* __restrict__ emb, int32_t* __restrict__ out,
+                                          const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid) {
+  const int n = __builtin_amdgcn_readfirstlane(sm.cnt[ql] + sm.cnt1[ql]);
+  if (FWAV_TOPK_SMALLSORT && C > 128 && n <= 128)
+    compact16_e<C, 2, SM>(kq, sm, ql, K, emb, out, sp, ties, qid);
+  else
+    compact16_e<C, C / 64, SM>(kq, sm, ql, K, emb, out, sp, ties, qid);
 }
 
 // End of a table piece (split block): no rescoring and no sort here — the piece keeps the entries of its band whose
@@ -1471,6 +1487,48 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
 // published Lk holds K entries above it, so the union has at least K whenever Lk != 0.  A query flagged by any piece,
 // or whose union would not fit one sort (C entries), goes to the exact-mode relaunch list once, seeded with the
 // largest flag key (each a valid band limit) or Lk.  One wave per query.
+// k_merge_pieces' last step: the band's mb ≤ 64·E keys (staged in LDS) rescored in exact f32 (sgemv16), sorted
+// (score desc, index asc), listed if tied, the first K emitted.
+template <int E>
+__device__ __forceinline__ void merge_band(const uint64_t* __restrict__ sw, int mb, int K, const float* __restrict__ emb,
+                                           int64_t qrow, const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid,
+                                           int32_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  uint64_t v[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    v[j] = e < mb ? sw[e] : 0ull;
+  }
+  const float4* qp = reinterpret_cast<const float4*>(emb + qrow * 16);
+  float qv[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 x = qp[i];
+    qv[4 * i] = x.x; qv[4 * i + 1] = x.y; qv[4 * i + 2] = x.z; qv[4 * i + 3] = x.w;
+  }
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    if (v[j] != 0ull) {
+      const int32_t d = key_idx(v[j]);
+      const float4* rp = reinterpret_cast<const float4*>(emb + (int64_t)d * 16);
+      float4 row[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) row[i] = rp[i];
+      const float acc = sgemv16([&](int k) { return f4c(row[k >> 2], k & 3); }, [&](int k) { return qv[k]; },
+                                sgemv_kind((uint32_t)d, sp));
+      v[j] = make_key(acc, d);
+    }
+  }
+  wave_sort_desc<E>(v);
+  record_tie<E>(ties, qid, tie_flags<E>(v, mb, K), v, mb, K, true);
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int e = j * 64 + lane;
+    if (e < K) out[e] = v[j] != 0ull ? key_idx(v[j]) : -1;
+  }
+}
+
 template <int C, int QB, bool HL>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
@@ -1553,12 +1611,6 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
       mb += __popcll(bm);
     }
   }
-  uint64_t v[E];
-#pragma unroll
-  for (int j = 0; j < E; ++j) {
-    const int e = j * 64 + lane;
-    v[j] = e < mb && e < C ? sw[e] : 0ull;  // same wave: its own ds_writes are ordered before these reads
-  }
   if (seed != 0u || mb > C) {
     if (lane == 0) {
       const int pos = atomicAdd(n_ovf, 1);
@@ -1567,34 +1619,11 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
     }
     return;
   }
-  const float4* qp = reinterpret_cast<const float4*>(emb + ((int64_t)qid + q_offset) * 16);
-  float qv[16];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float4 x = qp[i];
-    qv[4 * i] = x.x; qv[4 * i + 1] = x.y; qv[4 * i + 2] = x.z; qv[4 * i + 3] = x.w;
-  }
-#pragma unroll
-  for (int j = 0; j < E; ++j) {
-    if (v[j] != 0ull) {
-      const int32_t d = key_idx(v[j]);
-      const float4* rp = reinterpret_cast<const float4*>(emb + (int64_t)d * 16);
-      float4 row[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) row[i] = rp[i];
-      const float acc = sgemv16([&](int k) { return f4c(row[k >> 2], k & 3); }, [&](int k) { return qv[k]; },
-                                sgemv_kind((uint32_t)d, sp));
-      v[j] = make_key(acc, d);
-    }
-  }
-  wave_sort_desc<E>(v);
-  record_tie<E>(ties, qid, tie_flags<E>(v, mb < C ? mb : C, K), v, mb < C ? mb : C, K, true);
-  int32_t* out = cand + (int64_t)qid * K;
-#pragma unroll
-  for (int j = 0; j < E; ++j) {
-    const int e = j * 64 + lane;
-    if (e < K) out[e] = v[j] != 0ull ? key_idx(v[j]) : -1;
-  }
+  // same wave: its own ds_writes are ordered before merge_band's reads
+  if (FWAV_TOPK_SMALLSORT && C > 128 && mb <= 128)
+    merge_band<2>(sw, mb, K, emb, (int64_t)qid + q_offset, sp, ties, qid, cand + (int64_t)qid * K);
+  else
+    merge_band<E>(sw, mb, K, emb, (int64_t)qid + q_offset, sp, ties, qid, cand + (int64_t)qid * K);
 }
 
 // Host-side plan: default policy from the device's workgroup slots, or a diagnostic override.
