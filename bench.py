@@ -304,6 +304,11 @@ def main():
                      "launch_ms": t_topk * 1e3, "rank": rank},
         "stage_ms": stage_ms,
     }
+    if traffic:
+        # the north star's "fraction of the HBM roofline" for the same launch: measured HBM bytes (PMC) over its time
+        # (the kernel is bound by MFMA/VALU issue, not by HBM: its table is re-read from the Infinity Cache)
+        hbm = traffic / t_topk / 1e9
+        line["roofline"]["hbm"] = {"achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm / HBM_PEAK_GBS}
     if per_rank is not None:
         line["per_rank"] = per_rank
     extras = not sharded and not args.no_extras
