@@ -495,3 +495,12 @@ def test_sub_block_search_equals_single_launch(nsub):
             t = r.ties.cpu().numpy()
             return np.sort(t[1:1 + 9 * int(t[0])].reshape(-1, 9)[:, 0])
         assert np.array_equal(recs(got), recs(ref)), name
+        # a shard that starts mid-signal (a rank's block: query rows offset by lo)
+        lo, hi = ref.n_ranges // 5, ref.n_ranges - ref.n_ranges // 7
+        a = engine.compress_device(sig, p["tile"], k, energy_thresh=p["thr"], shard=(lo, hi), sub_blocks=1)
+        b = engine.compress_device(sig, p["tile"], k, energy_thresh=p["thr"], shard=(lo, hi), sub_blocks=nsub)
+        torch.cuda.synchronize()
+        assert (a.n_ties, a.n_resolved) == (b.n_ties, b.n_resolved), name
+        for nm in ("idx", "s", "o", "sym", "err"):
+            assert bit_equal(getattr(b, nm).cpu().numpy(), getattr(a, nm).cpu().numpy()), (name, "shard", nm)
+            assert bit_equal(getattr(b, nm).cpu().numpy(), getattr(ref, nm).cpu().numpy()[lo:hi]), (name, "rows", nm)
