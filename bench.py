@@ -9,7 +9,7 @@ Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
 path on the same single signal (strong scaling, "scaling": "strong"): rank 0 holds the signal in HBM, RCCL
 broadcasts it over xGMI, every rank rebuilds ranges/pool/embeddings, searches + solves its prune-balanced block of
 ranges, and the match arrays are gathered to rank 0 (fwav.dist.compress_sharded_start/finish).  The timed steps
-include every broadcast and gather; up to two calls are in flight, so a call's host tie ranking (defer_ties, as
+include every broadcast and gather; up to three calls are in flight, so a call's host tie ranking (defer_ties, as
 at N = 1) overlaps the next calls' searches before its gather; value = n_ranges / max-over-ranks step time.  N = 1
 is the same path with no collective (compress_device), so the driver's per-N values form a strong-scaling curve.
 
