@@ -16,8 +16,9 @@ from fwav import _lib  # noqa: E402
 from fwav._lib import call, size_call  # noqa: E402
 
 if os.environ.get("AB_LIB"):  # counters of another build (tools/ab_build.sh)
-    _lib.LIB_PATH = os.path.abspath(os.environ["AB_LIB"])
-    _lib._lib = None
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import _ablib
+    _ablib.use(os.environ["AB_LIB"])
 
 sig_h, _, _ = synth.make_config_signal("cfg2")
 sig = torch.from_numpy(sig_h).cuda()

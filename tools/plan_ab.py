@@ -16,8 +16,9 @@ from fwav._lib import call, size_call  # noqa: E402
 from fwav import _lib  # noqa: E402
 
 if os.environ.get("AB_LIB"):  # another build (tools/ab_build.sh)
-    _lib.LIB_PATH = os.path.abspath(os.environ["AB_LIB"])
-    _lib._lib = None
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import _ablib
+    _ablib.use(os.environ["AB_LIB"])
 
 plans = [tuple(int(x) for x in p.split(":")) for p in sys.argv[1].split(",")]
 secs = float(sys.argv[2]) if len(sys.argv) > 2 else 60.0

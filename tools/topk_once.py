@@ -15,8 +15,9 @@ from fwav import _lib  # noqa: E402
 from fwav._lib import call, size_call  # noqa: E402
 
 if os.environ.get("AB_LIB"):  # another build (tools/ab_build.sh), e.g. for PMC passes of a variant
-    _lib.LIB_PATH = os.path.abspath(os.environ["AB_LIB"])
-    _lib._lib = None
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import _ablib
+    _ablib.use(os.environ["AB_LIB"])
 
 dbg = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 sig = torch.from_numpy(synth.noise(60.0, 44100)).cuda()
