@@ -481,11 +481,19 @@ constexpr int kMaxPieces = 8;        // a split block's table pieces (merge: P·
 // P < 0 selects query halves instead of table pieces: each of the last R blocks becomes two items of half its
 // queries (W/2 waves, the other waves exit at once) that stream the whole table — no merge, no restarted limits, and a
 // half block on a CU of its own runs its waves faster than a full block.
+// Piece-major order (pm, when every block is split): item j is piece j / R of block j % R, so the first round runs
+// the first pieces of all blocks and a later piece of a block starts after its earlier pieces have published their
+// limits (A/B builds: FWAV_TOPK_PMAJOR=0 keeps block-major order everywhere).
+#ifndef FWAV_TOPK_PMAJOR
+#define FWAV_TOPK_PMAJOR 1
+#endif
 struct TopkPlan {
   int64_t nb, F, R;
   int P, qb;
-  bool halves;
+  bool halves, pm;
   __host__ __device__ int64_t items() const { return F + R * P; }
+  // the item of table piece p of split block b
+  __host__ __device__ int64_t item_of(int64_t b, int p) const { return pm ? F + (int64_t)p * R + (b - F) : F + (b - F) * P + p; }
 };
 __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, int qb) {
   TopkPlan pl;
@@ -495,6 +503,7 @@ __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, 
   pl.P = pl.halves ? 2 : (P < 1 ? 1 : (P > kMaxPieces ? kMaxPieces : P));
   pl.R = pl.P == 1 ? 0 : (pl.nb < rt ? pl.nb : (int64_t)rt);
   pl.F = pl.nb - pl.R;
+  pl.pm = FWAV_TOPK_PMAJOR && !pl.halves && pl.P > 1 && pl.F == 0 && pl.R > 0;
   return pl;
 }
 // Query (position in the active list) of slot ql = group·32 + col of query block `block`.  INTERLEAVE: a block's
@@ -522,6 +531,8 @@ __host__ __device__ inline void plan_item(const TopkPlan& pl, int64_t item, int6
     block = pl.F + j / pl.P;
     if (pl.halves) {
       piece = 0; np = 1; qhalf = (int)(j % 2);
+    } else if (pl.pm) {
+      block = pl.F + j % pl.R; piece = (int)(j / pl.R); np = pl.P;
     } else {
       piece = (int)(j % pl.P); np = pl.P;
     }
@@ -1554,7 +1565,7 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   cnt[0] = 0;
 #pragma unroll
   for (int p = 0; p < kMaxPieces; ++p) {
-    const int64_t item = plan.F + (block - plan.F) * P + (p < P ? p : 0);
+    const int64_t item = plan.item_of(block, p < P ? p : 0);
     kqs[p] = gkeys_all + ((size_t)item * QB + ql) * C;
     const uint64_t hdr = p < P ? kqs[p][C - 1] : 0ull;
     seed = max(seed, (uint32_t)(hdr >> 32));
@@ -1691,8 +1702,21 @@ static void host_plan_for(int64_t max_q, int64_t nd, bool wide, int& rt, int& P)
     rt = 0;
     P = 1;
     if (2 * nb <= slots) {
+      // every block split, pieces in piece-major order (TopkPlan::pm): the later pieces of a block start from the
+      // limits its earlier pieces published, so twice the pieces that fit one round pay (one process per
+      // configuration, identical outputs: 41,344 queries 3.60 → 3.35 ms with 6 pieces instead of 3 block-major;
+      // 65,536: 5.29 → 4.83 with 4 instead of 2; 20,672: 2.25 → 2.08 with 6, block-major before)
       rt = (int)nb;
-      P = (int)(slots / nb < kMaxPieces ? slots / nb : kMaxPieces);
+      int64_t p = slots / nb;
+      if (FWAV_TOPK_PMAJOR && p < 4) p *= 2;
+      P = (int)(p < kMaxPieces ? p : kMaxPieces);
+    } else if (FWAV_TOPK_PMAJOR && 3 * nb <= 2 * slots) {
+      // up to two thirds of the slots: every block in ⌊2·slots / nb⌋ ≥ 3 pieces, piece-major — two rounds, the
+      // second starting from the first's limits (82,688 queries: 6.43 → 5.92 ms with 3 pieces; the tail split below
+      // stays for more blocks: all of cfg2 in 2 / 3 piece-major pieces 20.8 / 20.5 vs 20.2–20.4 ms)
+      rt = (int)nb;
+      const int64_t p = 2 * slots / nb;
+      P = (int)(p < kMaxPieces ? p : kMaxPieces);
     } else {
       const int64_t last = nb % slots == 0 ? slots : nb % slots;  // blocks in the last round
       if (last > cus) {

@@ -73,11 +73,14 @@ def test_debug_search_rejects_workspace_of_another_query_count(lib):
     rejects a short one before any launch; the product always sizes for the query count it launches."""
     L = lib.lib()
     nd = 1_321_977
-    small, big_q = L.fwav_sim_topk_workspace_size(41344, nd, 64), L.fwav_sim_topk_workspace_size(20672, nd, 64)
-    assert big_q > small
+    sizes = {q: L.fwav_sim_topk_workspace_size(q, nd, 64) for q in (20672, 41344, 65536, 82688, 131072)}
+    # a workspace sized for more queries can be too small for fewer (their plan splits more blocks into pieces)
+    pairs = [(a, b) for a in sizes for b in sizes if b < a and sizes[b] > sizes[a]]
+    assert pairs, sizes
     p = ctypes.c_void_p(16)
-    rc = L.fwav_debug_sim_topk(p, p, nd, p, p, 20672, 0, 64, p, p, small, 0, None, None)
-    assert rc == -5 and b"workspace" in L.fwav_last_error()
+    for q, ws in [(pairs[0][1], sizes[pairs[0][0]]), (20672, sizes[20672] - 1)]:
+        rc = L.fwav_debug_sim_topk(p, p, nd, p, p, q, 0, 64, p, p, ws, 0, None, None)
+        assert rc == -5 and b"workspace" in L.fwav_last_error(), (q, ws)
 
 
 def test_library_digest_matches_sources(lib):
