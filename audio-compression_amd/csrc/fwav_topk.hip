@@ -1710,12 +1710,14 @@ static void host_plan_for(int64_t max_q, int64_t nd, bool wide, int& rt, int& P)
       int64_t p = slots / nb;
       if (FWAV_TOPK_PMAJOR && p < 4) p *= 2;
       P = (int)(p < kMaxPieces ? p : kMaxPieces);
-    } else if (FWAV_TOPK_PMAJOR && 3 * nb <= 2 * slots) {
-      // up to two thirds of the slots: every block in ⌊2·slots / nb⌋ ≥ 3 pieces, piece-major — two rounds, the
-      // second starting from the first's limits (82,688 queries: 6.43 → 5.92 ms with 3 pieces; the tail split below
-      // stays for more blocks: all of cfg2 in 2 / 3 piece-major pieces 20.8 / 20.5 vs 20.2–20.4 ms)
+    } else if (FWAV_TOPK_PMAJOR && 2 * nb <= 3 * slots) {
+      // up to 1.5 rounds of blocks: every block in max(3, ⌊2·slots / nb⌋) pieces, piece-major — later rounds start
+      // from the earlier pieces' limits (82,688 queries: 6.43 → 5.92 ms with 3 pieces; 165,375: 11.27 → 10.81 with
+      // 3, 10.72 with 4; the tail split below stays for more blocks: all of cfg2 in 2 / 3 / 4 piece-major pieces
+      // 20.8 / 20.5 / 20.7 vs 20.2–20.4 ms)
       rt = (int)nb;
-      const int64_t p = 2 * slots / nb;
+      int64_t p = 2 * slots / nb;
+      if (p < 3) p = 3;
       P = (int)(p < kMaxPieces ? p : kMaxPieces);
     } else {
       const int64_t last = nb % slots == 0 ? slots : nb % slots;  // blocks in the last round
