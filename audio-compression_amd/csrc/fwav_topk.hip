@@ -532,7 +532,9 @@ __host__ __device__ inline void plan_item(const TopkPlan& pl, int64_t item, int6
     if (pl.halves) {
       piece = 0; np = 1; qhalf = (int)(j % 2);
     } else if (pl.pm) {
-      block = pl.F + j % pl.R; piece = (int)(j / pl.R); np = pl.P;
+      // items past this plan (the grid covers the plan of max_q, the device count may be smaller) map to no block
+      block = j < pl.R * pl.P ? pl.F + j % pl.R : pl.nb;
+      piece = j < pl.R * pl.P ? (int)(j / pl.R) : 0; np = pl.P;
     } else {
       piece = (int)(j % pl.P); np = pl.P;
     }

@@ -504,3 +504,35 @@ def test_sub_block_search_equals_single_launch(nsub):
         for nm in ("idx", "s", "o", "sym", "err"):
             assert bit_equal(getattr(b, nm).cpu().numpy(), getattr(a, nm).cpu().numpy()), (name, "shard", nm)
             assert bit_equal(getattr(b, nm).cpu().numpy(), getattr(ref, nm).cpu().numpy()[lo:hi]), (name, "rows", nm)
+
+
+def test_pieces_plan_with_fewer_active_queries_than_launched():
+    """The search's grid and workspace cover the plan of max_q, while every workgroup re-derives the plan from the
+    device-side active count.  In the piece-major plan (every block split) the items past the smaller plan must do
+    nothing: the same active list searched with max_q = 11,025 and with max_q = its own count gives identical rows
+    (44 vs 20 blocks in 8 table pieces)."""
+    from fwav import synth
+    from fwav._lib import size_call
+    sig = td(synth.noise(2.0, 44100, seed=3))
+    from fwav import ties
+    r = engine.compress_device(sig, 2048, 64, keep_intermediates=True, tie_order="index")
+    torch.cuda.synchronize()
+    nd, nr = r.n_domains, r.n_ranges
+    st = torch.cuda.current_stream().cuda_stream
+    emb16 = torch.empty(size_call("fwav_emb16_elems", nd), dtype=torch.float16, device=dev())
+    call("fwav_emb16_from_emb", r.emb.data_ptr(), nd, emb16.data_ptr(), st)
+    nq = 5000
+    active = torch.arange(nq, dtype=torch.int32, device=dev())
+    n_active = torch.tensor([nq], dtype=torch.int32, device=dev())
+    out = {}
+    for max_q in (nr, nq):
+        wk = size_call("fwav_sim_topk_workspace_size", max_q, nd, 64)
+        ws = torch.empty(wk, dtype=torch.uint8, device=dev())
+        cand = torch.full((max_q * 64,), -7, dtype=torch.int32, device=dev())
+        call("fwav_sim_topk", r.emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), max_q,
+             0, 64, ties.blas_threads(), cand.data_ptr(), None, ws.data_ptr(), wk, st)
+        torch.cuda.synchronize()
+        out[max_q] = cand[:nq * 64].cpu().numpy()
+    assert np.array_equal(out[nr], out[nq])
+    assert (out[nq] >= 0).all() and (out[nq] < nd).all()
+    assert np.array_equal(out[nq].reshape(nq, 64), r.cand.view(-1, 64)[:nq].cpu().numpy())
