@@ -481,7 +481,7 @@ constexpr int kMaxPieces = 8;        // a split block's table pieces (merge: P·
 // P < 0 selects query halves instead of table pieces: each of the last R blocks becomes two items of half its
 // queries (W/2 waves, the other waves exit at once) that stream the whole table — no merge, no restarted limits, and a
 // half block on a CU of its own runs its waves faster than a full block.
-// Piece-major order (pm, when every block is split): item j is piece j / R of block j % R, so the first round runs
+// Piece-major order (pm) of the split blocks: split item j is piece j / R of block F + j % R, so the first round runs
 // the first pieces of all blocks and a later piece of a block starts after its earlier pieces have published their
 // limits (A/B builds: FWAV_TOPK_PMAJOR=0 keeps block-major order everywhere).
 #ifndef FWAV_TOPK_PMAJOR
@@ -503,7 +503,7 @@ __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, 
   pl.P = pl.halves ? 2 : (P < 1 ? 1 : (P > kMaxPieces ? kMaxPieces : P));
   pl.R = pl.P == 1 ? 0 : (pl.nb < rt ? pl.nb : (int64_t)rt);
   pl.F = pl.nb - pl.R;
-  pl.pm = FWAV_TOPK_PMAJOR && !pl.halves && pl.P > 1 && pl.F == 0 && pl.R > 0;
+  pl.pm = FWAV_TOPK_PMAJOR && !pl.halves && pl.P > 1 && pl.R > 0;
   return pl;
 }
 // Query (position in the active list) of slot ql = group·32 + col of query block `block`.  INTERLEAVE: a block's
@@ -1724,7 +1724,9 @@ static void host_plan_for(int64_t max_q, int64_t nd, bool wide, int& rt, int& P)
     } else {
       const int64_t last = nb % slots == 0 ? slots : nb % slots;  // blocks in the last round
       if (last > cus) {
-        rt = (int)(2 * (last - cus) < nb ? 2 * (last - cus) : nb);
+        // piece-major: the whole last round in 4 pieces (cfg2, one process per plan: 20.29–20.49 → 19.93 ms; the
+        // block-major plan split only its 2·(surplus) doubled-up blocks)
+        rt = (int)(FWAV_TOPK_PMAJOR ? last : (2 * (last - cus) < nb ? 2 * (last - cus) : nb));
         P = 4;
       } else if (5 * last <= 3 * cus) {
         // a last round of lone workgroups on at most 60 % of the CUs: its blocks as 4 table pieces each.  Same-box
