@@ -1734,6 +1734,9 @@ static void host_plan_for(int64_t max_q, int64_t nd, bool wide, int& rt, int& P)
         // of cfg2) 12.54 / 11.24, 200 12.60 / 12.74, 250 13.13 / 13.33
         rt = (int)last;
         P = 4;
+        // piece-major (base geometry): the round before it too, so that the short round's pieces follow pieces of
+        // their own blocks (cfg3, one process per plan: 177.1–177.6 → 175.3–175.7 ms)
+        if (FWAV_TOPK_PMAJOR && !wide && nb >= last + slots) rt = (int)(last + slots);
       }
     }
   }

@@ -22,22 +22,29 @@ if os.environ.get("AB_LIB"):  # another build (tools/ab_build.sh)
 
 plans = [tuple(int(x) for x in p.split(":")) for p in sys.argv[1].split(",")]
 secs = float(sys.argv[2]) if len(sys.argv) > 2 else 60.0
-sig = torch.from_numpy(synth.noise(secs, 44100)).cuda()
-r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
+cfgname = os.environ.get("AB_CFG")  # a BASELINE config (cfg3: speech-like, pruned active list) instead of noise
+if cfgname:
+    sig = torch.from_numpy(synth.make_config_signal(cfgname, seed=0)[0]).cuda()
+    tile = synth.CONFIGS[cfgname]["tile"]
+else:
+    sig = torch.from_numpy(synth.noise(secs, 44100)).cuda()
+    tile = 2048
+r = engine.compress_device(sig, tile, 64, keep_intermediates=True)
 torch.cuda.synchronize()
 nd, nr = r.n_domains, r.n_ranges
-emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
-tab = engine.embed_tables(8, torch.device("cuda"))
-pool = torch.empty(nd * 8, device="cuda")
-emb = torch.empty(nd * 16, device="cuda")
-ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
+emb = r.emb
+emb16 = torch.empty(size_call("fwav_emb16_elems", nd), dtype=torch.float16, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
-call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
-     emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
-nq = int(os.environ.get("AB_NQ", nr))
+call("fwav_emb16_from_emb", emb.data_ptr(), nd, emb16.data_ptr(), st)
 if os.environ.get("GEOM"):  # first-pass geometry override: 0 = base, 1 = wide
     call("fwav_debug_topk_geometry", int(os.environ["GEOM"]))
-active = torch.arange(nq, dtype=torch.int32, device="cuda")
+if cfgname:
+    nq = int(r.n_active.item())
+    active = r.active[:nq].clone()
+    nr = max(nr, nq)
+else:
+    nq = int(os.environ.get("AB_NQ", nr))
+    active = torch.arange(nq, dtype=torch.int32, device="cuda")
 n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
 ref = None
 res = []
@@ -46,7 +53,7 @@ for rnd in range(3):
         call("fwav_debug_topk_plan", rt, P)
         wsn = size_call("fwav_sim_topk_workspace_size", nq, nd, 64)
         wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
-        cand = torch.empty(nq * 64, dtype=torch.int32, device="cuda")
+        cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")  # rows are indexed by range (active[i])
         ts = []
         for _ in range(3):
             e0 = torch.cuda.Event(enable_timing=True)
@@ -59,9 +66,10 @@ for rnd in range(3):
             ts.append(e0.elapsed_time(e1))
         o = wsn - 4 - 4 * max(nq, 1)  # workspace tail: first pass's overflow list, its count, then u32 seeds[q]
         n_ovf = int(wsk[o:o + 4].view(torch.int32).item())
+        rows = cand.view(-1, 64)[active.long()]  # only the searched rows are written
         if ref is None:
-            ref = cand.clone()
-        same = bool(torch.equal(cand, ref))
+            ref = rows.clone()
+        same = bool(torch.equal(rows, ref))
         if rnd == 2:
             res.append((rt, P, np.median(ts), min(ts), same, wsn, n_ovf))
         del wsk
