@@ -128,12 +128,16 @@ class DeviceCompressed:
     n_resolved: int = 0      # of those, rows re-ranked with numpy's own tie order (fwav.ties)
     empty: bool = False
     pending: Optional[object] = None  # deferred tie resolution (compress_device(defer_ties=True)): a Future
+    apply: Optional[object] = None    # ... and its last step, run by wait() on the caller's current stream
 
     def wait(self) -> "DeviceCompressed":
         """Complete a deferred tie resolution (no-op otherwise); the outputs are final afterwards."""
         if self.pending is not None:
-            self.pending.result()
+            staged = self.pending.result()
             self.pending = None
+            if staged is not None and self.apply is not None:
+                self.apply(*staged)
+            self.apply = None
         return self
 
     def is_silent(self) -> bool:
@@ -291,10 +295,18 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
         _mark(events, "prune")
         sc = float(abs(F32(s_clip)))
         nsub = 1
-        if tie_order != "index" and not defer_ties:
-            nsub = int(sub_blocks) if sub_blocks is not None else _tie_sub_blocks(m, nd)
+        sliced = False
+        if tie_order != "index":
+            if sub_blocks is not None:
+                nsub = int(sub_blocks)
+            elif not defer_ties or nd >= SUB_BLOCK_MIN_DOMAINS:
+                nsub = _tie_sub_blocks(m, nd)
             nsub = max(1, min(nsub, m))
-        if nsub == 1:
+            # large tables, deferred: the sliced path too (even as one slice), so that the exact score rows are
+            # queued right after the search instead of behind the next call's (the driver thread's side stream
+            # would wait for it), and only the copies, numpy's ranking and the fix-up are deferred
+            sliced = nsub > 1 or (defer_ties and nd >= SUB_BLOCK_MIN_DOMAINS)
+        if not sliced:
             _mark(events, "sim_topk")
             wk = size_call("fwav_sim_topk_workspace_size", m, nd, k) if (emb16 is not None or k > 64) else 0
             wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
@@ -307,7 +319,7 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
             call("fwav_affine", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, sc, idx.data_ptr(),
                  s.data_ptr(), o.data_ptr(), sym.data_ptr(), err.data_ptr(), st)
             _mark(events, "affine")
-        if nsub == 1 and ties is not None:
+        if not sliced and ties is not None:
             # exactly tied scores whose order can change a match: numpy's own ranking for those rows (fwav.ties)
             _mark(events, "ties")
             resolve = torch.empty(m + 1, dtype=torch.int32, device=dev)
@@ -322,14 +334,32 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
                                        threads=threads, ranges=rsh, range_size=rs, pool=pool, s_clip=sc, cand=cand,
                                        outs=(idx, s, o, sym, err), stream=stream_id)
 
+            def stage(stream_id):
+                # deferred: on the driver thread, the counts, the exact score rows and their copies; numpy's ranking
+                # then runs on the host pool while the driver moves on to the next call, and wait() applies it
+                counts = torch.stack([ties[0], resolve[0]]).cpu()
+                res.n_ties, res.n_resolved = int(counts[0]), int(counts[1])
+                if not res.n_resolved:
+                    return None
+                rows = resolve[1:1 + res.n_resolved]
+                futs = _ties.rank_rows(_ties.score_row_launches(rows, emb=emb, n_domains=nd, q_offset=lo,
+                                                                threads=threads, stream=stream_id),
+                                       res.n_resolved, nd, k)
+                return rows, futs
+
+            def apply(rows, futs):
+                _ties.apply_rows(rows, futs, ranges=rsh, range_size=rs, pool=pool, n_domains=nd, k=k, s_clip=sc,
+                                 cand=cand, outs=(idx, s, o, sym, err), stream=_stream(dev))
+
             if defer_ties:
-                res.pending = _ties.defer(finish, dev)
+                res.apply = apply
+                res.pending = _ties.defer(stage, dev)
             else:
                 finish(st)
             _mark(events, "ties")
-        elif nsub > 1:
+        elif sliced:
             ties = _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb16, active, n_active,
-                                      rsh, pool, cand, (idx, s, o, sym, err), res, events, st)
+                                      rsh, pool, cand, (idx, s, o, sym, err), res, events, st, defer=defer_ties)
     res.pool, res.idx, res.s, res.o, res.sym, res.err, res.n_active = pool, idx, s, o, sym, err, n_active
     if keep_intermediates:
         res.ranges, res.emb, res.cand, res.active = ranges, emb, cand, active
@@ -362,8 +392,18 @@ def _slice_bounds(m: int, nsub: int) -> list[tuple[int, int]]:
     return [(cuts[j], cuts[j + 1]) for j in range(nsub) if cuts[j + 1] > cuts[j]]
 
 
+class _Staged:
+    """A deferred sliced tie resolution: the slices' (rows, future of their ranking) pairs (DeviceCompressed.wait)."""
+
+    def __init__(self, pend):
+        self.pend = pend
+
+    def result(self):
+        return (self.pend,)
+
+
 def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb16, active, n_active, rsh, pool, cand,
-                       outs, res, events, st):
+                       outs, res, events, st, defer=False):
     """The search as ``nsub`` launches over consecutive slices of the active list.  After each slice's search and tie
     check the host reads its tie counts (one synchronisation), queues the exact score rows of its tied rows and hands
     their copies and numpy's ranking to the driver thread (fwav.ties.rank_rows_async); then the next slice searches.
@@ -405,12 +445,18 @@ def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb1
     call("fwav_affine", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, sc, *[t.data_ptr() for t in outs],
          st)
     _mark(events, "affine")
-    _mark(events, "ties")
-    for rows, fut in pend:
-        _ties.apply_rows(rows, fut.result(), ranges=rsh, range_size=rs, pool=pool, n_domains=nd, k=k, s_clip=sc,
-                         cand=cand, outs=outs, stream=st)
-    _mark(events, "ties")
+    def apply(pend_):
+        for rows, fut in pend_:
+            _ties.apply_rows(rows, fut.result(), ranges=rsh, range_size=rs, pool=pool, n_domains=nd, k=k, s_clip=sc,
+                             cand=cand, outs=outs, stream=_stream(dev))
+
     res.n_ties, res.n_resolved = n_ties, n_res
+    if defer:  # wait() applies the rankings on the caller's stream
+        res.pending, res.apply = _Staged(pend), apply
+    else:
+        _mark(events, "ties")
+        apply(pend)
+        _mark(events, "ties")
     # one tie list in fwav_sim_topk's layout (count, then the records of every slice)
     return torch.cat([torch.tensor([n_ties], dtype=torch.int32, device=dev)] + lists)
 

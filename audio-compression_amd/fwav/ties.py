@@ -96,8 +96,8 @@ def _driver():
 
 def defer(finish, device: torch.device):
     """Run ``finish(stream)`` — the host half of a tie resolution — on the background driver thread, on a side stream
-    that first waits for everything queued so far on ``device``'s current stream.  Returns its Future.  One driver
-    thread: resolutions run in call order."""
+    that first waits for everything queued so far on ``device``'s current stream.  Returns the Future of its result.
+    One driver thread: resolutions run in call order."""
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(device))
     key = str(device)
@@ -110,8 +110,9 @@ def defer(finish, device: torch.device):
     def job():
         with torch.cuda.device(device), torch.cuda.stream(side):
             side.wait_event(ev)
-            finish(side.cuda_stream)
+            out = finish(side.cuda_stream)
             side.synchronize()
+            return out
 
     return _driver().submit(job)
 

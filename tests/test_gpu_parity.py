@@ -483,7 +483,13 @@ def test_sub_block_search_equals_single_launch(nsub):
                                      sub_blocks=1)
         got = engine.compress_device(sig, p["tile"], k, energy_thresh=p["thr"], keep_intermediates=True,
                                      sub_blocks=nsub)
+        # deferred: the slices' rankings applied by wait()
+        dfr = engine.compress_device(sig, p["tile"], k, energy_thresh=p["thr"], sub_blocks=nsub, defer_ties=True)
+        dfr.wait()
         torch.cuda.synchronize()
+        assert (dfr.n_ties, dfr.n_resolved) == (ref.n_ties, ref.n_resolved), name
+        for nm in ("idx", "s", "o", "sym", "err"):
+            assert bit_equal(getattr(dfr, nm).cpu().numpy(), getattr(ref, nm).cpu().numpy()), (name, "deferred", nm)
         if name == "tone":
             assert ref.n_resolved > 0
         assert (got.n_ties, got.n_resolved) == (ref.n_ties, ref.n_resolved), name
