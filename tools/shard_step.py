@@ -60,7 +60,7 @@ def main():
             for _ in range(a.steps):
                 inflight.append(engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard,
                                                        defer_ties=True))
-                while len(inflight) > 2:
+                while len(inflight) > 3:  # three calls in flight, as bench.py
                     inflight.pop(0).wait()
             for x in inflight:
                 x.wait()
