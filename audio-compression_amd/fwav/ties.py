@@ -237,7 +237,9 @@ def apply_rows(rows: torch.Tensor, futs: list, *, ranges: torch.Tensor, range_si
     rows into ``outs`` = (idx, s, o, sym, err), on the current stream (``stream``)."""
     dev = rows.device
     n = rows.numel()
-    newc = torch.from_numpy(np.stack([f.result() for f in futs])).to(dev)
+    # through page-locked memory, asynchronously: a copy from pageable memory would first wait for everything queued
+    # on the stream (in a stream of calls, the calls still in flight)
+    newc = torch.from_numpy(np.stack([f.result() for f in futs])).pin_memory().to(dev, non_blocking=True)
     ridx = rows.long()
     cand.view(-1, k)[ridx] = newc
     rs = int(range_size)
