@@ -24,7 +24,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--ns", default="1,2,4,8", help="world sizes to simulate")
+    ap.add_argument("--ranks", default="", help="only these ranks (comma list; default every rank)")
+    ap.add_argument("--lags", default="3", help="calls in flight for the pipelined loop (comma list: one column each)")
     a = ap.parse_args()
+    lags = [int(x) for x in a.lags.split(",")]
     import __graft_entry__
     __graft_entry__.build()
     from fwav import dist as fdist
@@ -35,11 +39,11 @@ def main():
     sig = torch.from_numpy(sig_h).to(dev)
     tile, K = cfg["tile"], cfg["top_k"]
     out = {}
-    for N in (1, 2, 4, 8):
+    for N in [int(x) for x in a.ns.split(",")]:
         per = []
         rg, nr_, rs_ = engine.ranges_device(sig, tile, 1e-4)
         blocks = fdist.prune_balanced_bounds(rg, nr_, rs_, 1e-4, N)
-        for rank in range(N):
+        for rank in ([int(x) for x in a.ranks.split(",") if int(x) < N] if a.ranks else range(N)):
             # the bench computes these bounds every step on a side stream, off the critical path (fwav.dist); here
             # they are computed once, so that the timed loop has no host synchronisation either
             shard = blocks[rank]
@@ -55,25 +59,30 @@ def main():
             torch.cuda.synchronize()
             wall = (time.perf_counter() - t0) / a.steps * 1e3
             st = {k: float(np.mean([e[k][0].elapsed_time(e[k][1]) for e in evs])) for k in evs[0]}
-            inflight = []
-            t0 = time.perf_counter()
-            for _ in range(a.steps):
-                inflight.append(engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard,
-                                                       defer_ties=True))
-                while len(inflight) > 3:  # three calls in flight, as bench.py
-                    inflight.pop(0).wait()
-            for x in inflight:
-                x.wait()
-            torch.cuda.synchronize()
-            pipe = (time.perf_counter() - t0) / a.steps * 1e3
+            pipes = {}
+            for lag in lags:
+                inflight = []
+                t0 = time.perf_counter()
+                for _ in range(a.steps):
+                    inflight.append(engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard,
+                                                           defer_ties=True))
+                    while len(inflight) > lag:  # calls in flight (bench.py: 3)
+                        inflight.pop(0).wait()
+                for x in inflight:
+                    x.wait()
+                torch.cuda.synchronize()
+                pipes[lag] = (time.perf_counter() - t0) / a.steps * 1e3
+            pipe = pipes[lags[0]]
             per.append({"rank": rank, "ranges": r.shard[1] - r.shard[0], "tie_rows": r.n_resolved,
-                        "wall_ms_sync": wall, "wall_ms_pipelined": pipe, "stage_ms": st})
+                        "wall_ms_sync": wall, "wall_ms_pipelined": pipe,
+                        "wall_ms_pipelined_by_lag": pipes, "stage_ms": st})
         out[N] = {"max_wall_ms_sync": max(p["wall_ms_sync"] for p in per),
                   "max_wall_ms_pipelined": max(p["wall_ms_pipelined"] for p in per), "ranks": per}
         print(N, json.dumps(out[N]), flush=True)
-    print(json.dumps({N: {"speedup_sync": out[1]["max_wall_ms_sync"] / v["max_wall_ms_sync"],
-                          "speedup_pipelined": out[1]["max_wall_ms_pipelined"] / v["max_wall_ms_pipelined"]}
-                      for N, v in out.items()}), flush=True)
+    if 1 in out:
+        print(json.dumps({N: {"speedup_sync": out[1]["max_wall_ms_sync"] / v["max_wall_ms_sync"],
+                              "speedup_pipelined": out[1]["max_wall_ms_pipelined"] / v["max_wall_ms_pipelined"]}
+                          for N, v in out.items()}), flush=True)
 
 if __name__ == "__main__":
     main()
