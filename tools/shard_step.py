@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8", help="world sizes to simulate")
     ap.add_argument("--ranks", default="", help="only these ranks (comma list; default every rank)")
     ap.add_argument("--lags", default="3", help="calls in flight for the pipelined loop (comma list: one column each)")
+    ap.add_argument("--tie-order", default="numpy", help="compress_device tie_order (index: no host tie step)")
     a = ap.parse_args()
     lags = [int(x) for x in a.lags.split(",")]
     import __graft_entry__
@@ -48,13 +49,14 @@ def main():
             # they are computed once, so that the timed loop has no host synchronisation either
             shard = blocks[rank]
             for _ in range(2):
-                engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard)
+                engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard, tie_order=a.tie_order)
             torch.cuda.synchronize()
             evs = []
             t0 = time.perf_counter()
             for _ in range(a.steps):
                 ev = {}
-                r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard, events=ev)
+                r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard, events=ev,
+                                           tie_order=a.tie_order)
                 evs.append(ev)
             torch.cuda.synchronize()
             wall = (time.perf_counter() - t0) / a.steps * 1e3
@@ -65,7 +67,7 @@ def main():
                 t0 = time.perf_counter()
                 for _ in range(a.steps):
                     inflight.append(engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard,
-                                                           defer_ties=True))
+                                                           defer_ties=True, tie_order=a.tie_order))
                     while len(inflight) > lag:  # calls in flight (bench.py: 3)
                         inflight.pop(0).wait()
                 for x in inflight:
