@@ -499,6 +499,34 @@ __global__ __launch_bounds__(256) void k_gather_rows(const float4* __restrict__ 
   if (acc == 1.2345f) out[0] = acc;
 }
 
+
+// Tie fix-up (fwav.ties.apply_rows): numpy-ranked candidate rows in, the affine re-solve's five outputs out, each
+// in one launch instead of a gather/scatter per array.  One wave per row in; one thread per row out.
+__global__ __launch_bounds__(64) void k_tie_rows_in(const int32_t* __restrict__ rows, const int32_t* __restrict__ new_cand,
+                                                    int K, int32_t* __restrict__ cand, const float* __restrict__ ranges,
+                                                    int rs, float* __restrict__ ranges_out) {
+  const int64_t i = blockIdx.x;
+  const int64_t r = rows[i];
+  for (int t = threadIdx.x; t < K; t += 64) cand[r * K + t] = new_cand[i * K + t];
+  for (int t = threadIdx.x; t < rs; t += 64) ranges_out[i * rs + t] = ranges[r * rs + t];
+}
+
+__global__ __launch_bounds__(256) void k_tie_rows_out(const int32_t* __restrict__ rows, int64_t n,
+                                                      const int32_t* __restrict__ idx_in, const float* __restrict__ s_in,
+                                                      const float* __restrict__ o_in, const uint8_t* __restrict__ sym_in,
+                                                      const float* __restrict__ err_in, int32_t* __restrict__ idx,
+                                                      float* __restrict__ s, float* __restrict__ o,
+                                                      uint8_t* __restrict__ sym, float* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+  idx[r] = idx_in[i];
+  s[r] = s_in[i];
+  o[r] = o_in[i];
+  sym[r] = sym_in[i];
+  err[r] = err_in[i];
+}
+
 }  // namespace fwav
 
 using namespace fwav;
@@ -570,6 +598,30 @@ int fwav_affine(const float* ranges, int64_t nr, int rs, const int32_t* cand, in
       k_affine_any<<<grid, thr, 0, st>>>(ranges, nr, rs, cand, K, pool, s_clip, out_idx, out_s, out_o, out_sym, out_err);
   }
   FWAV_LAUNCH_CHECK("fwav_affine");
+  return FWAV_OK;
+}
+
+int fwav_tie_rows_in(const int32_t* rows, int64_t n, const int32_t* new_cand, int K, int32_t* cand,
+                     const float* ranges, int rs, float* ranges_out, void* stream) {
+  FWAV_CHECK_ARG(n == 0 || (rows && new_cand && cand && ranges && ranges_out), FWAV_ERR_ARG,
+                 "fwav_tie_rows_in: null pointer");
+  FWAV_CHECK_ARG(n >= 0 && K >= 1 && rs >= 1, FWAV_ERR_SHAPE, "fwav_tie_rows_in: bad shape");
+  if (n == 0) return FWAV_OK;
+  k_tie_rows_in<<<n, 64, 0, (hipStream_t)stream>>>(rows, new_cand, K, cand, ranges, rs, ranges_out);
+  FWAV_LAUNCH_CHECK("fwav_tie_rows_in");
+  return FWAV_OK;
+}
+
+int fwav_tie_rows_out(const int32_t* rows, int64_t n, const int32_t* idx_in, const float* s_in, const float* o_in,
+                      const uint8_t* sym_in, const float* err_in, int32_t* out_idx, float* out_s, float* out_o,
+                      uint8_t* out_sym, float* out_err, void* stream) {
+  FWAV_CHECK_ARG(n == 0 || (rows && idx_in && s_in && o_in && sym_in && err_in && out_idx && out_s && out_o && out_sym &&
+                            out_err), FWAV_ERR_ARG, "fwav_tie_rows_out: null pointer");
+  FWAV_CHECK_ARG(n >= 0, FWAV_ERR_SHAPE, "fwav_tie_rows_out: bad shape");
+  if (n == 0) return FWAV_OK;
+  k_tie_rows_out<<<cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(rows, n, idx_in, s_in, o_in, sym_in, err_in, out_idx,
+                                                               out_s, out_o, out_sym, out_err);
+  FWAV_LAUNCH_CHECK("fwav_tie_rows_out");
   return FWAV_OK;
 }
 

@@ -50,6 +50,8 @@ SIGNATURES = {
     "fwav_debug_gather_rows": (I32, [P, I64, I32, I64, P, P]),
     "fwav_affine": (I32, [P, I64, I32, P, I32, P, I64, F32, P, P, P, P, P, P]),
     "fwav_tie_check": (I32, [P, I64, I32, P, I32, P, I64, P, I64, I32, P, I64, I32, P, P]),
+    "fwav_tie_rows_in": (I32, [P, I64, P, I32, P, P, I32, P, P]),
+    "fwav_tie_rows_out": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P]),
     "fwav_tie_list_size": (I64, [I64]),
     "fwav_emb16_from_emb": (I32, [P, I64, P, P]),
     "fwav_debug_topk_plan_info": (I32, [I64, I64, P, P]),

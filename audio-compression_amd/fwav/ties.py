@@ -240,15 +240,16 @@ def apply_rows(rows: torch.Tensor, futs: list, *, ranges: torch.Tensor, range_si
     # through page-locked memory, asynchronously: a copy from pageable memory would first wait for everything queued
     # on the stream (in a stream of calls, the calls still in flight)
     newc = torch.from_numpy(np.stack([f.result() for f in futs])).pin_memory().to(dev, non_blocking=True)
-    ridx = rows.long()
-    cand.view(-1, k)[ridx] = newc
+    rows = rows.contiguous()
     rs = int(range_size)
-    rsub = ranges.view(-1, rs)[ridx].contiguous()
+    rsub = torch.empty(n * rs, dtype=torch.float32, device=dev)
+    # three launches: candidate rows scattered + their ranges gathered, the affine re-solve, the outputs scattered
+    call("fwav_tie_rows_in", rows.data_ptr(), n, newc.data_ptr(), k, cand.data_ptr(), ranges.data_ptr(), rs,
+         rsub.data_ptr(), stream)
     tmp = [torch.empty(n, dtype=t.dtype, device=dev) for t in outs]
     call("fwav_affine", rsub.data_ptr(), n, rs, newc.data_ptr(), k, pool.data_ptr(), int(n_domains), float(s_clip),
          *[t.data_ptr() for t in tmp], stream)
-    for t, u in zip(outs, tmp):
-        t[ridx] = u
+    call("fwav_tie_rows_out", rows.data_ptr(), n, *[t.data_ptr() for t in tmp], *[t.data_ptr() for t in outs], stream)
 
 
 def resolve_rows(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, k: int, threads: int,

@@ -173,6 +173,16 @@ int fwav_affine(const float* ranges, int64_t n_ranges, int range_size, const int
 int fwav_tie_check(const float* ranges, int64_t n_ranges, int range_size, const int32_t* cand, int k,
                    const float* pool, int64_t n_domains, const float* emb, int64_t q_offset, int blas_threads,
                    const int32_t* ties, int64_t max_ties, int exact_sets, int32_t* resolve, void* stream);
+/* Tie fix-up, in (fwav.ties.apply_rows): for j < n, row r = rows[j] (local index): cand[r·k ..] = new_cand[j·k ..]
+ * (numpy's ranking of row r, fractal.py:537-541) and ranges_out[j·rs ..] = ranges[r·rs ..], the compact input of
+ * the fwav_affine re-solve of those rows. */
+int fwav_tie_rows_in(const int32_t* rows, int64_t n, const int32_t* new_cand, int k, int32_t* cand,
+                     const float* ranges, int range_size, float* ranges_out, void* stream);
+/* Tie fix-up, out: the re-solve's compact outputs (j < n) scattered to row rows[j] of the five output arrays
+ * (fractal.py:816-870 for those rows). */
+int fwav_tie_rows_out(const int32_t* rows, int64_t n, const int32_t* idx_in, const float* s_in, const float* o_in,
+                      const uint8_t* sym_in, const float* err_in, int32_t* out_idx, float* out_s, float* out_o,
+                      uint8_t* out_sym, float* out_err, void* stream);
 /* Diagnostic (bench roofline, not the product path): n uniformly random rows of rs floats (rs 4/8/16, 16-B aligned
  * table of n_rows rows) gathered with nothing computed — the ceiling of fwav_affine's memory side on this device.
  * sink: one float of device memory. */
