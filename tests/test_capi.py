@@ -65,6 +65,15 @@ def test_error_codes_without_gpu(lib):
     assert rc == -1
     rc = L.fwav_score_rows(None, 100, None, 1, 0, 1, None, None)
     assert rc == -1
+    # tie fix-up: null arrays with rows to apply are rejected; no rows is a no-op (no launch)
+    rc = L.fwav_tie_rows_in(None, 3, None, 64, None, None, 8, None, None)
+    assert rc == -1 and b"fwav_tie_rows_in" in L.fwav_last_error()
+    assert L.fwav_tie_rows_in(None, 0, None, 64, None, None, 8, None, None) == 0
+    rc = L.fwav_tie_rows_out(None, 3, *[None] * 10, None)
+    assert rc == -1 and b"fwav_tie_rows_out" in L.fwav_last_error()
+    assert L.fwav_tie_rows_out(None, 0, *[None] * 10, None) == 0
+    rc = L.fwav_tie_rows_in(big, -1, big, 64, big, big, 8, big, None)
+    assert rc == -2  # FWAV_ERR_SHAPE
 
 
 def test_debug_search_rejects_workspace_of_another_query_count(lib):
