@@ -128,15 +128,25 @@ class DeviceCompressed:
     n_resolved: int = 0      # of those, rows re-ranked with numpy's own tie order (fwav.ties)
     empty: bool = False
     pending: Optional[object] = None  # deferred tie resolution (compress_device(defer_ties=True)): a Future
-    apply: Optional[object] = None    # ... and its last step, run by wait() on the caller's current stream
+    apply: Optional[object] = None    # ... and its last step, run by wait() on the call's own stream
+    stream: Optional[object] = None   # the torch stream the call's kernels were queued on
 
     def wait(self) -> "DeviceCompressed":
-        """Complete a deferred tie resolution (no-op otherwise); the outputs are final afterwards."""
+        """Complete a deferred tie resolution (no-op otherwise); the outputs are final afterwards.  The fix-up runs on
+        the call's own stream, after its search and affine solve, and whichever stream is current here waits for it
+        (so both the call's stream and the caller's see final outputs)."""
         if self.pending is not None:
             staged = self.pending.result()
             self.pending = None
             if staged is not None and self.apply is not None:
-                self.apply(*staged)
+                st = self.stream if self.stream is not None else torch.cuda.current_stream()
+                caller = torch.cuda.current_stream(st.device)
+                with torch.cuda.device(st.device), torch.cuda.stream(st):
+                    self.apply(*staged)
+                if caller != st:
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    caller.wait_event(ev)
             self.apply = None
         return self
 
@@ -249,7 +259,8 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     wsen = torch.empty(wse, dtype=torch.uint8, device=dev)
     call("fwav_weighted_energy", ranges.data_ptr(), n, partial.data_ptr(), wsen.data_ptr(), wse, st)
     _mark(events, "voiced_ranges")
-    res = DeviceCompressed(nr, rs, tile_size, step, energy_thresh, n, nd, k, (0, nr), energy_partial=partial)
+    res = DeviceCompressed(nr, rs, tile_size, step, energy_thresh, n, nd, k, (0, nr), energy_partial=partial,
+                           stream=torch.cuda.current_stream(dev))
     if n < tile_size or nr > nd:
         # the reference returns the empty tuple for silent input before it ever builds domains
         if res.is_silent() or n < tile_size:

@@ -13,6 +13,7 @@ Layout (little-endian, packed):
 from __future__ import annotations
 
 import hashlib
+import os
 import struct
 import wave
 from concurrent.futures import ThreadPoolExecutor
@@ -160,6 +161,19 @@ def load_compressed(filepath, verify_checksum=True):
          original_len) = struct.unpack(HEADER_FMT, f.read(HEADER_SIZE))
         stored = f.read(32)
         sha = _Hasher() if verify_checksum else None
+        need = 4 * range_size * n_domains + MATCH_DTYPE.itemsize * n_ranges
+        if os.fstat(f.fileno()).st_size - f.tell() < need:
+            # a truncated (or hostile) header: no allocation from its counts; the checksum still decides first, as
+            # in the reference, which hashes whatever follows the header
+            if sha is not None:
+                while True:
+                    piece = f.read(_CHUNK)
+                    if not piece:
+                        break
+                    sha.update(piece)
+                if sha.digest() != stored:
+                    raise ValueError("Checksum mismatch — file may be corrupted")
+            raise ValueError("truncated FWAV file")
         domains = np.empty((n_domains, range_size), np.float32)
         rec = np.empty(n_ranges, MATCH_DTYPE)
         got_d = _read_into(f, domains, sha)

@@ -36,30 +36,61 @@ MAX_SLOTS = 64
 #: sub-block's rows in one launch, so that none waits behind the next sub-block's search
 PIPE_ROW_BUDGET = 16 << 30
 
-_BLAS_THREADS = None
+_BLAS_GET = None
 _TRACE = bool(os.environ.get("FWAV_TIES_TRACE"))
+
+#: get_num_threads entry points of the OpenBLAS builds numpy ships with (scipy-openblas64, scipy-openblas32, plain)
+_OPENBLAS_GET = ("scipy_openblas_get_num_threads64_", "scipy_openblas_get_num_threads", "openblas_get_num_threads64_",
+                 "openblas_get_num_threads")
+
+
+def _openblas_libs() -> list:
+    """Candidate files of the OpenBLAS that numpy's ``@`` calls: the one numpy's wheel bundles (``numpy.libs``), else
+    the OpenBLAS builds threadpoolctl finds loaded in this process."""
+    import glob
+    root = os.path.dirname(os.path.dirname(np.__file__))
+    libs = sorted(glob.glob(os.path.join(root, "numpy.libs", "*openblas*")))
+    if libs:
+        return libs
+    try:
+        import threadpoolctl
+        return sorted({i["filepath"] for i in threadpoolctl.threadpool_info() if i.get("internal_api") == "openblas"})
+    except ImportError:
+        return []
 
 
 def blas_threads() -> int:
-    """OpenBLAS's thread count in this process — the split of the reference's sgemv that decides which domains its
-    tail kernels score (fwav_common.h).  The reference would run here with the same numpy, so its scores follow this
-    count; ``FWAV_BLAS_THREADS`` overrides it."""
-    global _BLAS_THREADS
+    """OpenBLAS's thread count in this process, read from numpy's own OpenBLAS (its ``get_num_threads``) at every
+    call — the split of the reference's sgemv (fractal.py:537) that decides which domains its tail kernels score
+    (fwav_common.h).  The reference would run here with the same numpy, so its scores follow this count.
+    ``FWAV_BLAS_THREADS`` overrides it.  Raises FwavError when the count cannot be read (no guess: a wrong count
+    silently changes which columns take the tail kernels' order)."""
+    global _BLAS_GET
     env = os.environ.get("FWAV_BLAS_THREADS")
     if env:
         return max(1, int(env))
-    if _BLAS_THREADS is None:
-        n = None
-        try:
-            import threadpoolctl
-            for info in threadpoolctl.threadpool_info():
-                if info.get("user_api") == "blas":
-                    n = int(info["num_threads"])
+    if _BLAS_GET is None:
+        import ctypes
+        libs = _openblas_libs()
+        found = []
+        for path in libs:
+            h = ctypes.CDLL(path)  # already loaded by numpy: the same handle, so the count is numpy's live one
+            for sym in _OPENBLAS_GET:
+                if hasattr(h, sym):
+                    f = getattr(h, sym)
+                    f.restype, f.argtypes = ctypes.c_int, []
+                    found.append(f)
                     break
-        except Exception:  # noqa: BLE001
-            n = None
-        _BLAS_THREADS = max(1, n if n else (os.cpu_count() or 1))
-    return _BLAS_THREADS
+        if len(found) != 1:
+            from ._lib import FwavError
+            raise FwavError(f"cannot read numpy's OpenBLAS thread count ({len(found)} OpenBLAS builds found in {libs});"
+                            " set FWAV_BLAS_THREADS to the reference's thread count")
+        _BLAS_GET = found[0]
+    n = int(_BLAS_GET())
+    if n < 1:
+        from ._lib import FwavError
+        raise FwavError(f"numpy's OpenBLAS reports {n} threads")
+    return n
 
 
 def numpy_topk_row(scores: np.ndarray, k: int) -> np.ndarray:
@@ -207,15 +238,19 @@ def rank_rows(launches, n: int, n_domains: int, k: int, copy_stream=None) -> lis
 
 
 def rank_rows_async(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, k: int, threads: int,
-                    stream: int):
-    """Queue every exact score row of ``rows`` now (one launch per PIPE_ROW_BUDGET), and copy + rank them on the
-    driver thread (copies on a copy stream that waits for the launches).  Returns a Future of the n row futures.
-    Used between the query sub-blocks of one search (fwav.engine), so that the next sub-block's search does not
-    delay the score rows: only their copies and numpy's ranking overlap it."""
+                    stream: int, budget: int = PIPE_ROW_BUDGET):
+    """Queue the exact score rows of ``rows`` now — at most ``budget`` bytes of them, in one launch — and copy + rank
+    them on the driver thread (copies on a copy stream that waits for the launches).  Returns a Future of the n row
+    futures.  Used between the query sub-blocks of one search (fwav.engine), so that the next sub-block's search does
+    not delay the score rows: only their copies and numpy's ranking overlap it.  Rows beyond the budget (a periodic
+    input can tie thousands of rows, 345 MB each at cfg4) are launched lazily by the driver thread, one budget at a
+    time as the earlier ones reach the host, so the device holds at most ``budget`` bytes of score rows per slice."""
     n = rows.numel()
-    launches = list(score_row_launches(rows, emb=emb, n_domains=n_domains, q_offset=q_offset, threads=threads,
-                                       stream=stream, budget=PIPE_ROW_BUDGET))
     dev = rows.device
+    cur = torch.cuda.current_stream(dev)  # the launches' stream (``stream``): their events are recorded on it
+    gen = score_row_launches(rows, emb=emb, n_domains=n_domains, q_offset=q_offset, threads=threads, stream=stream,
+                             budget=budget)
+    first = [next(gen)] if n else []
     key = str(dev)
     if key not in _COPY:
         _COPY[key] = torch.cuda.Stream(dev)
@@ -223,8 +258,10 @@ def rank_rows_async(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_
 
     def job():
         def it():  # each launch's scores are released once its rows are on the host
-            while launches:
-                yield launches.pop(0)
+            while first:
+                yield first.pop(0)
+            with torch.cuda.stream(cur):
+                yield from gen
         with torch.cuda.device(dev):
             return rank_rows(it(), n, n_domains, k, copy_stream=cs)
 

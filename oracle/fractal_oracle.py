@@ -264,16 +264,27 @@ def zero_query_candidates(nd: int, k: int) -> np.ndarray:
 
 
 def blas_threads() -> int:
-    """OpenBLAS's thread count in this process (what numpy's sgemv would split over; sgemv_col_kind)."""
-    try:
-        import threadpoolctl
-        for info in threadpoolctl.threadpool_info():
-            if info.get("user_api") == "blas":
-                return int(info["num_threads"])
-    except Exception:
-        pass
+    """OpenBLAS's thread count in this process (what numpy's sgemv would split over; sgemv_col_kind), read from the
+    OpenBLAS numpy bundles (its get_num_threads).  Raises when it cannot be read — never a guess."""
+    import ctypes
+    import glob
     import os
-    return os.cpu_count() or 1
+    root = os.path.dirname(os.path.dirname(np.__file__))
+    libs = sorted(glob.glob(os.path.join(root, "numpy.libs", "*openblas*")))
+    if not libs:
+        import threadpoolctl
+        libs = sorted({i["filepath"] for i in threadpoolctl.threadpool_info() if i.get("internal_api") == "openblas"})
+    got = []
+    for path in libs:
+        h = ctypes.CDLL(path)
+        for sym in ("scipy_openblas_get_num_threads64_", "scipy_openblas_get_num_threads",
+                    "openblas_get_num_threads64_", "openblas_get_num_threads"):
+            if hasattr(h, sym):
+                got.append(int(getattr(h, sym)()))
+                break
+    if len(got) != 1 or got[0] < 1:
+        raise RuntimeError(f"cannot read numpy's OpenBLAS thread count from {libs}")
+    return got[0]
 
 
 #: OpenBLAS (interface/gemv.c) runs sgemv single-threaded while m·n < 115200·GEMM_MULTITHREAD_THRESHOLD (= 4)

@@ -56,6 +56,21 @@ def test_load_compressed_roundtrip_and_errors(tmp_path):
     with pytest.raises(ValueError, match="Checksum mismatch"):
         load_compressed(str(bad))
     load_compressed(str(bad), verify_checksum=False)
+    # a header whose counts promise more bytes than the file holds (truncated or hostile): no allocation from the
+    # counts; a short payload fails its checksum first, as in the reference, which hashes whatever follows the header
+    from fwav.fwavio import HEADER_FMT
+    fields = list(struct.unpack(HEADER_FMT, raw[:struct.calcsize(HEADER_FMT)]))
+    fields[9] = 0xFFFFFFFF  # n_domains: 4 Gi domain rows (32 GiB at range_size 2)
+    huge = struct.pack(HEADER_FMT, *fields) + raw[struct.calcsize(HEADER_FMT):]
+    bad.write_bytes(huge)  # (the checksum covers the payload only, so it still matches)
+    for verify in (True, False):
+        with pytest.raises(ValueError, match="truncated FWAV file"):
+            load_compressed(str(bad), verify_checksum=verify)
+    bad.write_bytes(raw[:-5])
+    with pytest.raises(ValueError, match="Checksum mismatch"):
+        load_compressed(str(bad))
+    with pytest.raises(ValueError, match="truncated FWAV file"):
+        load_compressed(str(bad), verify_checksum=False)
 
 
 def test_empty_fwav_cannot_be_loaded(tmp_path):

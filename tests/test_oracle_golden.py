@@ -119,3 +119,42 @@ def test_smooth_matches_numpy_convolve():
             e = (rng.random(n) * rng.choice([1e-5, 1e-2, 1.0, 1e3], n)).astype(np.float32)
             ref = np.convolve(e, np.full(w, np.float32(1) / np.float32(w), np.float32), mode="same")
             assert np.array_equal(O.smooth5(e, w).view(np.uint32), ref.view(np.uint32)), (w, n)
+
+
+def _unit_head_rows(rng, nd):
+    """Rows shaped like the reference's embeddings: tonal dims 0-7 and transient dims 8-15 each of unit norm."""
+    e = rng.standard_normal((nd, 16)).astype(np.float32)
+    for h in (slice(0, 8), slice(8, 16)):
+        e[:, h] /= np.sqrt((e[:, h].astype(np.float64) ** 2).sum(1)).astype(np.float32)[:, None]
+    return e
+
+
+@pytest.mark.parametrize("nd", [28_801, 1_321_977])
+def test_sgemv_thread_split_pinned_against_numpy(nd):
+    """The reference's scores ``domain_embs @ q`` (fractal.py:537) above OpenBLAS's threading threshold
+    (16·nd ≥ 460,800, i.e. nd ≥ 28,800: every config from cfg2 up): OpenBLAS splits the columns over its T threads and
+    each thread scores its chunk's last columns with the 4x2 / 4x1 tail kernels.  The oracle's split
+    (sgemv_col_kind) and per-kind order (sgemv_scores) must equal numpy's own ``E @ q`` bit-for-bit on every column
+    for T ∈ {1, 2, 3, 5, 8, 16}, under threadpoolctl's limit — and fwav.ties.blas_threads() must read back that T
+    from numpy's OpenBLAS.  A wrong T must be caught: the T = 1 split disagrees with numpy at T = 8."""
+    threadpoolctl = pytest.importorskip("threadpoolctl")
+    from fwav import ties
+
+    rng = np.random.default_rng(nd)
+    e = _unit_head_rows(rng, nd)
+    qi = rng.integers(0, nd, 4)
+    cols = np.arange(nd)
+    refs = {}
+    for T in (1, 2, 3, 5, 8, 16):
+        with threadpoolctl.threadpool_limits(T, user_api="blas"):
+            assert ties.blas_threads() == T
+            assert O.blas_threads() == T
+            refs[T] = np.stack([e @ e[i] for i in qi])
+        got = O.sgemv_scores(e, e[qi], O.sgemv_col_kind(cols, nd, T))
+        assert np.array_equal(got.view(np.uint32), refs[T].view(np.uint32)), (nd, T)
+    if nd == 1_321_977:
+        # the thread split is observable: scoring with T = 1's kernels misses numpy's T = 8 bits somewhere
+        k1, k8 = O.sgemv_col_kind(cols, nd, 1), O.sgemv_col_kind(cols, nd, 8)
+        assert (k1 != k8).sum() == 20
+        wrong = O.sgemv_scores(e, e[qi], k1)
+        assert not np.array_equal(wrong.view(np.uint32), refs[8].view(np.uint32))
