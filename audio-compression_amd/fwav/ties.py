@@ -186,6 +186,7 @@ def score_row_launches(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int,
         ev = torch.cuda.Event()
         ev.record()
         yield b0, S, ev
+        del S, ev  # not held while the next launch allocates: one launch's rows on the device at a time
 
 
 def rank_rows(launches, n: int, n_domains: int, k: int, copy_stream=None) -> list:
