@@ -432,6 +432,20 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_WPE
 #define FWAV_TOPK_WPE 4  // launch bound: waves per SIMD the register allocation must allow
 #endif
+// Centroid geometry (cent_level1): FWAV_TOPK_CENT query sets per wave (0: off), FWAV_TOPK_CW waves per
+// workgroup, FWAV_TOPK_CG chunks per barrier, FWAV_TOPK_CWPE waves per SIMD for the register allocation
+#ifndef FWAV_TOPK_CENT
+#define FWAV_TOPK_CENT 0
+#endif
+#ifndef FWAV_TOPK_CW
+#define FWAV_TOPK_CW 8
+#endif
+#ifndef FWAV_TOPK_CG
+#define FWAV_TOPK_CG 4
+#endif
+#ifndef FWAV_TOPK_CWPE
+#define FWAV_TOPK_CWPE 2
+#endif
 // Ablation builds (tools/ab_build.sh NAME -DFWAV_TOPK_ABL=<dbg bits>): the production kernel with the given `dbg`
 // bits fixed at compile time — the STATS kernel's counters cost registers (it spills), which skews its timings.
 #ifndef FWAV_TOPK_ABL
@@ -582,7 +596,7 @@ __device__ __forceinline__ bool may_pass(int imx, float thf) {
 
 // NG = query groups of 32 per workgroup (W waves × QS sets).  Kept small: two workgroups (2 × 64 KB of chunk
 // slots + this) must fit one CU's 160 KB of LDS.
-template <int NG, bool STATS>
+template <int NG, bool STATS, bool FIFO = true>
 struct Topk16SmemT {
   int cnt[32 * NG];   // final pass: entries at the front of the query's buffer (its h = 0 lane's appends)
   int cnt1[32 * NG];  // ... and at the back (its h = 1 lane's)
@@ -592,7 +606,7 @@ struct Topk16SmemT {
   uint32_t tie[32 * NG];
   int64_t qrow[32 * NG];
   int32_t qpos[32 * NG];  // position of the slot's query in the active list (index of its shared band limit)
-  uint32_t fired[NG][kFifo];                       // deferred work: ring of fired chunk entries
+  uint32_t fired[FIFO ? NG : 1][kFifo];            // deferred work: ring of fired chunk entries (not in CENT)
   unsigned long long wstat[STATS ? NG : 1][kStats];  // STATS builds only (one row per wave)
 };
 
@@ -1222,8 +1236,146 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
   }
 }
 
-template <int C, bool STATS, int MODE, int W = k16Waves, int G = kGroup, int QS = k16Sets>
-__global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TOPK_WPE) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
+// f(std::integral_constant<int, I>) for I = 0 .. N−1: loops over per-set register arrays with compile-time indices
+// where the body is too large for the unroller
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+// ---- Centroid pre-filter (CENT geometry): QS query sets of 32 per wave, one centroid per QS consecutive queries.
+// Centroid column j of a wave belongs to set j % QS and stands for its members, the columns QS·(j / QS) + k (k < QS)
+// of that set — QS consecutive positions of the active list, i.e. (unpruned) ranges a few samples apart, whose
+// embeddings lie close together.  With c the centroid's fp16 vector and ρ_h = max over members |q_hi,h − c_h| per
+// head h (the tonal and transient halves of the embedding, each of norm ≤ 1 in the table), every member's fp16 score
+// obeys s16(q, d) = (q_hi − c)·d_hi + c·d_hi ≤ s16(c, d) + (ρ_0 + ρ_1)(1 + 2⁻⁹) + 1e-5 (d_hi's heads have norm
+// ≤ 1 + 2⁻¹¹; both MFMA accumulations ≤ 16 roundings of ≤ 2).  So one MFMA of the 32 centroids per 32-domain tile
+// — a 4:1 (QS = 4) reduction of the fold, the stream's issue bound — decides which sets need their own MFMA and fold
+// for that tile: a set is scored only where some centroid of it reaches the smallest member threshold minus the
+// centroid's slack.  Exact: a tile skipped for a set holds no domain above any member's threshold.
+#ifdef FWAV_TOPK_CENTSTATS
+__device__ unsigned long long g_cent_stats[4];  // experiment builds: level-1 tiles, level-2 (tile, set) pairs
+#endif
+template <int QS>
+__device__ __forceinline__ uint64_t cent_set_mask(int s) {
+  static_assert(QS == 2 || QS == 4 || QS == 8, "centroid sets: 2, 4 or 8 query sets per wave");
+  constexpr uint64_t m = QS == 2 ? 0x5555555555555555ull : (QS == 4 ? 0x1111111111111111ull : 0x0101010101010101ull);
+  return m << s;
+}
+// The lane's centroid (column col = lane & 31, half h = lane >> 5): the fp16 mean of its members' query fragments and
+// the slack (ρ_0 + ρ_1)(1 + 2⁻⁹) + 1e-5 added to every member bound.  `qrow_of(k)` = member k's table row, or −1.
+template <int QS, class RowOf>
+__device__ __forceinline__ void centroid_setup(const _Float16* __restrict__ emb16, RowOf qrow_of, half8& bc,
+                                               float& slack) {
+  typedef float floatx8 __attribute__((ext_vector_type(8)));
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  auto frag = [&](int64_t r) {  // the member's fp16 high parts of head h (re-read from L2 in the second pass)
+    return *reinterpret_cast<const half8*>(emb16 + (((r >> 8) * 2 + h) * 256 + (r & 255)) * 8);
+  };
+  floatx8 sum = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int nv = 0;
+#pragma unroll
+  for (int k = 0; k < QS; ++k) {
+    const int64_t r = qrow_of(k);
+    if (r >= 0) {
+      const half8 m = frag(r);
+      ++nv;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sum[i] += (float)m[i];
+    }
+  }
+  half8 c;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) c[i] = (_Float16)(nv > 0 ? sum[i] / (float)nv : 0.0f);
+  float rho = 0.0f;
+#pragma unroll
+  for (int k = 0; k < QS; ++k) {
+    const int64_t r = qrow_of(k);
+    if (r >= 0) {
+      const half8 m = frag(r);
+      float d2 = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = (float)m[i] - (float)c[i];  // exact: a difference of two fp16 values
+        d2 += d * d;
+      }
+      rho = fmaxf(rho, __builtin_sqrtf(d2));
+    }
+  }
+  rho += __shfl_xor(rho, 32);  // both heads
+  bc = c;
+  slack = rho * (1.0f + 0x1p-9f) + 1e-5f;
+}
+// The lane's centroid filter threshold: the smallest stream threshold (float) of its members minus the slack
+// (+∞ when no member takes appends; −∞ members make the centroid fire on every tile).
+template <int QS>
+__device__ __forceinline__ int centroid_threshold(const float (&tv)[QS], float slack) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 31;
+  const int sj = col % QS, base = (lane & 32) + QS * (col / QS);
+  float mn = INFINITY;
+#pragma unroll
+  for (int k = 0; k < QS; ++k) {
+    float v = INFINITY;
+#pragma unroll
+    for (int s = 0; s < QS; ++s) {
+      const float x = __shfl(tv[s], base + k);
+      v = s == sj ? x : v;
+    }
+    mn = fminf(mn, v);
+  }
+  return int_threshold(mn - slack);
+}
+// Level 1 of the centroid pre-filter over one group of NC chunks: the 32 centroids scored against every tile (the
+// stream's software pipeline: fragments 3 tiles ahead, MFMAs one tile ahead); pend[s] bit i marks tile i of the group
+// where some centroid of set s reaches its threshold.  The marked (tile, set) pairs are then scored with the set's
+// own queries and their survivors appended at once (k_sim_topk_f16, CENT): no fired-chunk ring, no replay.
+template <int NC, int QS>
+__device__ __forceinline__ void cent_level1(const _Float16* __restrict__ lda0, half8 bc, int thc,
+                                            uint64_t (&pend)[QS]) {
+  constexpr int NT = 8 * NC;
+  static_assert(NT <= 64, "tile masks are 64-bit");
+  constexpr int kChunkHalfs = 512 * 8;
+  auto rd = [&](int i) {
+    return *reinterpret_cast<const half8*>(lda0 + (i >> 3) * kChunkHalfs + (i & 7) * 256);
+  };
+#pragma unroll
+  for (int s = 0; s < QS; ++s) pend[s] = 0ull;
+  half8 a[NT];
+  floatx16 acc[NT];
+#pragma unroll
+  for (int i = 0; i < 3 && i < NT; ++i) a[i] = rd(i);
+  acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bc, floatx16{}, 0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    if (i + 3 < NT) a[i + 3] = rd(i + 3);
+    if (i + 1 < NT) acc[i + 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i + 1], bc, floatx16{}, 0, 0, 0);
+    const uint64_t m = __ballot(fold16((int)0x80000000, acc[i]) > thc);
+#pragma unroll
+    for (int s = 0; s < QS; ++s)
+      if (m & cent_set_mask<QS>(s)) pend[s] |= 1ull << i;
+  }
+#ifdef FWAV_TOPK_CENTSTATS
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long np = 0;
+#pragma unroll
+    for (int s = 0; s < QS; ++s) np += __popcll(pend[s]);
+    atomicAdd(&g_cent_stats[0], (unsigned long long)NT);
+    atomicAdd(&g_cent_stats[1], np);
+  }
+#endif
+#ifdef FWAV_TOPK_CENT_L2OFF
+#pragma unroll
+  for (int s = 0; s < QS; ++s) pend[s] = 0ull;
+#endif
+}
+
+template <int C, bool STATS, int MODE, int W = k16Waves, int G = kGroup, int QS = k16Sets, bool CENT = false>
+__global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ? FWAV_TOPK_CWPE : FWAV_TOPK_WPE)) void k_sim_topk_f16(const _Float16* __restrict__ emb16,
                                                                 const float* __restrict__ emb, int64_t nd,
                                                                 const int32_t* __restrict__ active,
                                                                 const int32_t* __restrict__ n_active_p,
@@ -1245,11 +1397,11 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
   // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
   struct Lds {
     u32x4 slots[2 * G][512];
-    Topk16SmemT<NG, STATS> sm;
+    Topk16SmemT<NG, STATS, !CENT> sm;
   };
   __shared__ __attribute__((aligned(16))) Lds lds_all;
   u32x4(*slots)[512] = lds_all.slots;
-  Topk16SmemT<NG, STATS>& sm = lds_all.sm;
+  Topk16SmemT<NG, STATS, !CENT>& sm = lds_all.sm;
 
   const int n_active = *n_active_p;
   constexpr int QB = 32 * NG;  // queries per block
@@ -1347,6 +1499,15 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
     for (int s = 0; s < QS; ++s)
       if (upd[s]) thf[s] = fmaxf(thf[s], inseed[s]);
   }
+  half8 bc{};          // CENT: the lane's centroid (fp16, MFMA B operand) ...
+  float cslack = 0.0f;  // ... and its slack
+  if constexpr (CENT) {
+    const int sj = col % QS, mcol0 = QS * (col / QS);
+    centroid_setup<QS>(emb16, [&](int k) -> int64_t {
+      const int64_t qi = slot_query(block, qslot0 + (wave * QS + sj) * 32 + mcol0 + k, plan.nb, QB);
+      return qi < n_active ? (int64_t)active[qi] + q_offset : (int64_t)-1;
+    }, bc, cslack);
+  }
   const int nchunks = (int)cdiv(nd, kChunk);  // < 2^31 / 256: chunk arithmetic stays 32-bit (scalar)
   // this item's chunk range [c0, c1) (the whole table unless the block is split)
   const int c0 = (int)((int64_t)nchunks * piece / npieces), c1 = (int)((int64_t)nchunks * (piece + 1) / npieces);
@@ -1413,7 +1574,46 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
 #pragma unroll
     for (int s = 0; s < QS; ++s) thi[s] = int_threshold(HL ? thf[s] - kStreamMargin : thf[s]);
     const _Float16* lda0 = reinterpret_cast<const _Float16*>(half[0]) + ((h * kChunk) + col) * 8;
-    if (ABL && (dbg & (512 | 1024)) && c_end - cg == G) {
+    if constexpr (CENT) {
+      float tv[QS];
+#pragma unroll
+      for (int s = 0; s < QS; ++s) tv[s] = HL ? thf[s] - kStreamMargin : thf[s];
+      const int thc = centroid_threshold<QS>(tv, cslack);
+      uint64_t pend[QS];
+      if (c_end - cg == G) {
+        cent_level1<G, QS>(lda0, bc, thc, pend);
+      } else {
+#pragma unroll
+        for (int s = 0; s < QS; ++s) pend[s] = 0ull;
+        for (int c = cg; c < c_end; ++c) {
+          uint64_t pc[QS];
+          cent_level1<1, QS>(lda0 + (c - cg) * 512 * 8, bc, thc, pc);
+#pragma unroll
+          for (int s = 0; s < QS; ++s) pend[s] |= pc[s] << (8 * (c - cg));
+        }
+      }
+      // level 2: each marked (tile, set) scored with the set's queries; survivors appended now (the tile is in LDS)
+      static_for<QS>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        uint64_t pm = pend[s];
+        while (pm != 0ull) {
+          const int t = __builtin_ctzll(pm);
+          pm &= pm - 1;
+          const half8 af = *reinterpret_cast<const half8*>(lda0 + (t >> 3) * (512 * 8) + (t & 7) * 256);
+          floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, b[s], floatx16{}, 0, 0, 0);
+          const int64_t dt = (int64_t)(cg + (t >> 3)) * kChunk + (t & 7) * 32;
+          if constexpr (HL) {  // shl = s16 + d_hi·q_lo + d_lo·q_hi, refined only where some s16 can pass
+            if (__ballot(fold16((int)0x80000000, acc) > thi[s]) == 0ull) continue;
+            const half8 afl = tile_fragment(emb16lo, dt, h, col);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl, b[s], acc, 0, 0, 0);
+          }
+          thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(acc, thf[s], qcnt[s], kept[s], dt, nd,
+                                                                             gkeys, sm, wave * QS + s, K, upd[s],
+                                                                             stats, sp, emb, qv[s], &kth[s], share);
+        }
+      });
+    } else if (ABL && (dbg & (512 | 1024)) && c_end - cg == G) {
       // ablations 512: fold without ballots, 1024: MFMA without fold (outputs invalid)
       if (dbg & 1024)
         stream_group<G, QS, 2>(lda0, b, thi, cg, sm.fired + wave * QS, nfired, lane, &sink);
@@ -1435,14 +1635,17 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : FWAV_TO
           if (upd[s] && v != 0u) thf[s] = fmaxf(thf[s], key2f(v));
         }
       }
-      // each wave replays its own fired chunks (compacting inline when a buffer fills)
-#pragma unroll
-      for (int s = 0; s < QS; ++s) {
-        if (nfired[s] > cur[s].head || cur[s].rem != 0u)
-          thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s], qcnt[s], kept[s], cur[s],
-                                           nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s], stats, sp, emb, qv[s], &kth[s],
-                                           share);
-      }
+      // each wave replays its own fired chunks (compacting inline when a buffer fills); compile-time set indices
+      // (static_for): a runtime-indexed per-set array would live in scratch / LDS
+      static_for<QS>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        if constexpr (!CENT) {
+          if (nfired[s] > cur[s].head || cur[s].rem != 0u)
+            thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s],
+                                             qcnt[s], kept[s], cur[s], nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s],
+                                             stats, sp, emb, qv[s], &kth[s], share);
+        }
+      });
       if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
       // retire the replay's loads and stores here, visibly to hipcc's wait bookkeeping (vmcnt(0) expcnt(7)
       // lgkmcnt(15)): otherwise it keeps them "pending" at the loop head and waits on them before the next
@@ -1662,24 +1865,38 @@ static int current_device() {
 #endif
 constexpr int kWideW = 16, kWideG = 8;
 constexpr int kWideQB = 32 * kWideW;
-static int g_wide = -1;  // fwav_debug_topk_geometry (tests): force base / wide
-static bool wide_geometry(int64_t nd) { return g_wide >= 0 ? g_wide != 0 : nd > (int64_t)FWAV_TOPK_WIDE_MIN; }
+constexpr int kCentQS = FWAV_TOPK_CENT > 0 ? FWAV_TOPK_CENT : 4, kCentW = FWAV_TOPK_CW, kCentG = FWAV_TOPK_CG;
+constexpr int kCentQB = 32 * kCentW * kCentQS;
+static int g_wide = -1;  // fwav_debug_topk_geometry (tests): force base / wide / centroid
+// first-pass geometries
+constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2;
+static int first_geometry(int64_t nd) {
+  if (g_wide >= 0) return g_wide;
+  if (nd > (int64_t)FWAV_TOPK_WIDE_MIN) return kGeoWide;
+  return FWAV_TOPK_CENT > 0 ? kGeoCent : kGeoBase;
+}
+static bool wide_geometry(int64_t nd) { return first_geometry(nd) == kGeoWide; }
+static int geometry_qb(int geo) { return geo == kGeoWide ? kWideQB : (geo == kGeoCent ? kCentQB : k16QB); }
 
-static void topk_device_slots(bool wide, int& cus, int& per_cu) {
-  static int cs[2][kMaxDev] = {{0}}, ws[2][kMaxDev] = {{0}};
+static void topk_device_slots(int geo, int& cus, int& per_cu) {
+  static int cs[3][kMaxDev] = {{0}}, ws[3][kMaxDev] = {{0}};
   const int dev = current_device();
-  int& c = cs[wide][dev];
-  int& w = ws[wide][dev];
+  int& c = cs[geo][dev];
+  int& w = ws[geo][dev];
   if (c == 0) {
     const hipError_t occ =
-        wide ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeHL, kWideW, kWideG, 1>,
-                                                            64 * kWideW, 0)
-             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeS16>, 64 * k16Waves,
-                                                            0);
+        geo == kGeoWide
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeHL, kWideW, kWideG, 1>,
+                                                           64 * kWideW, 0)
+        : geo == kGeoCent
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                  &w, k_sim_topk_f16<k16Cap, false, kModeS16, kCentW, kCentG, kCentQS, true>, 64 * kCentW, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeS16>, 64 * k16Waves,
+                                                           0);
     if (!(hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && occ == hipSuccess &&
           c > 0 && w > 0)) {
       c = 256;  // MI355X: 256 CUs × 2 base (1 wide) workgroups
-      w = wide ? 1 : 2;
+      w = geo == kGeoBase ? 2 : 1;
     }
   }
   cus = c;
@@ -1692,15 +1909,16 @@ static void topk_device_slots(bool wide, int& cus, int& per_cu) {
 // fill in beside the lone workgroups (cfg2 A/B: 24.9 → 22.6 ms; splitting more blocks costs more than it saves,
 // since every piece restarts the rising limit: 268 blocks in 2 pieces 24.2 ms, 512 in 2 25.3 ms).  Few blocks
 // (at most half the slots) are each split into up to 8 pieces so that the table passes use the idle CUs.
-static void host_plan_for(int64_t max_q, int64_t nd, bool wide, int& rt, int& P) {
+static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
+  const bool wide = geo == kGeoWide;
   if (g_plan_rt >= 0) {  // diagnostic override
     rt = g_plan_rt;
     P = g_plan_p;
   } else {
     int cus, per_cu;
-    topk_device_slots(wide, cus, per_cu);
+    topk_device_slots(geo, cus, per_cu);
     const int64_t slots = (int64_t)cus * per_cu;
-    const int64_t nb = cdiv(max_q > 0 ? max_q : 1, wide ? kWideQB : k16QB);
+    const int64_t nb = cdiv(max_q > 0 ? max_q : 1, geometry_qb(geo));
     rt = 0;
     P = 1;
     if (2 * nb <= slots) {
@@ -1736,7 +1954,7 @@ static void host_plan_for(int64_t max_q, int64_t nd, bool wide, int& rt, int& P)
         P = 4;
         // piece-major (base geometry): the round before it too, so that the short round's pieces follow pieces of
         // their own blocks (cfg3, one process per plan: 177.1–177.6 → 175.3–175.7 ms)
-        if (FWAV_TOPK_PMAJOR && !wide && nb >= last + slots) rt = (int)(last + slots);
+        if (FWAV_TOPK_PMAJOR && geo == kGeoBase && nb >= last + slots) rt = (int)(last + slots);
       }
     }
   }
@@ -1749,10 +1967,10 @@ static void host_plan_for(int64_t max_q, int64_t nd, bool wide, int& rt, int& P)
 static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
   const int64_t q = max_q > 0 ? max_q : 1;
   size_t items_q = (size_t)make_plan(q, 0, 1, k16QB).items() * k16QB;
-  for (int wide = 0; wide < 2; ++wide) {
+  for (int geo = 0; geo < 3; ++geo) {
     int rt, P;
-    host_plan_for(q, nd, wide != 0, rt, P);
-    const int qb = wide ? kWideQB : k16QB;
+    host_plan_for(q, nd, geo, rt, P);
+    const int qb = geometry_qb(geo);
     const size_t n = (size_t)make_plan(q, rt, P, qb).items() * qb;
     items_q = n > items_q ? n : items_q;
   }
@@ -1794,18 +2012,26 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     // 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms — an even 4 waves per SIMD beats a fuller last round of workgroups.
     const bool stats_first = (stats != nullptr && !(dbg & (1 << 17))) || (dbg & 65535) != 0;
     // counter (STATS) builds of the first pass exist in the base geometry only
-    const bool wide = !stats_first && wide_geometry(nd);
+    const int geo = stats_first ? kGeoBase : first_geometry(nd);
+    const bool wide = geo == kGeoWide;
     int rt, P;
-    host_plan_for(max_q, nd, wide, rt, P);
-    const TopkPlan pl = make_plan(max_q, rt, P, wide ? kWideQB : k16QB);
+    host_plan_for(max_q, nd, geo, rt, P);
+    const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(geo));
     if (pl.R > 0 && !pl.halves) (void)hipMemsetAsync(share, 0, (size_t)q1 * sizeof(uint32_t), st);
     const int mode1 = first_mode(nd);
+#ifndef FWAV_TOPK_PADLDS
+#define FWAV_TOPK_PADLDS 0  // experiment builds: dynamic LDS added to the base first pass (caps its occupancy)
+#endif
 #define FWAV_FIRST(MODE_, STATS_, DBG_, ST_)                                                                    \
-  k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, 0, st>>>(                                 \
+  k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, FWAV_TOPK_PADLDS, st>>>(                  \
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, DBG_, ST_,  \
       sp, ties)
 #define FWAV_FIRST_WIDE(MODE_)                                                                                   \
   k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG, 1><<<pl.items(), 64 * kWideW, 0, st>>>(                    \
+      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
+      sp, ties)
+#define FWAV_FIRST_CENT(MODE_)                                                                                   \
+  k_sim_topk_f16<k16Cap, false, MODE_, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(        \
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
       sp, ties)
 #ifdef FWAV_TOPK_EXTSEED
@@ -1818,17 +2044,22 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       else FWAV_FIRST(kModeS16, true, dbg & 65535, stats);
     } else if (wide) {
       if (mode1 == kModeHL) FWAV_FIRST_WIDE(kModeHL); else FWAV_FIRST_WIDE(kModeS16);
+    } else if (geo == kGeoCent) {
+      if (mode1 == kModeHL) FWAV_FIRST_CENT(kModeHL); else FWAV_FIRST_CENT(kModeS16);
     } else {
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, nullptr); else FWAV_FIRST(kModeS16, false, 0, nullptr);
     }
 #undef FWAV_FIRST
 #undef FWAV_FIRST_WIDE
+#undef FWAV_FIRST_CENT
     if (pl.R > 0) {
 #define FWAV_MERGE(QB_, HL_)                                                                                    \
   k_merge_pieces<k16Cap, QB_, HL_><<<cdiv(pl.R * QB_, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, \
                                                                        ovf1, n_ovf1, share, emb, q_offset, sp, ties)
       if (wide) {
         if (mode1 == kModeHL) FWAV_MERGE(kWideQB, true); else FWAV_MERGE(kWideQB, false);
+      } else if (geo == kGeoCent) {
+        if (mode1 == kModeHL) FWAV_MERGE(kCentQB, true); else FWAV_MERGE(kCentQB, false);
       } else {
         if (mode1 == kModeHL) FWAV_MERGE(k16QB, true); else FWAV_MERGE(k16QB, false);
       }
@@ -1950,6 +2181,16 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t nd, const i
                           (hipStream_t)stream, (uint64_t*)workspace, make_sgemv_split(nd, 1), nullptr, dbg, stats);
 }
 
+#ifdef FWAV_TOPK_CENTSTATS
+// experiment builds: read and clear the centroid pre-filter's counters
+int fwav_debug_cent_stats(unsigned long long* host) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cent_stats), 4 * sizeof(unsigned long long));
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_cent_stats), z, sizeof(z));
+  return FWAV_OK;
+}
+#endif
 #ifdef FWAV_TOPK_DEBUG
 int fwav_debug_dump(void* host, size_t bytes, unsigned* n_events) {
   (void)hipDeviceSynchronize();
@@ -1969,7 +2210,7 @@ int fwav_debug_topk_mode(int mode) {
 // Diagnostic override of the first pass's geometry: 0 = base (8 waves, 256 queries per workgroup), 1 = wide (16
 // waves, 512 queries, one workgroup per CU), −1 = by table size (default).  Both return the same candidates.
 int fwav_debug_topk_geometry(int wide) {
-  FWAV_CHECK_ARG(wide >= -1 && wide <= 1, FWAV_ERR_ARG, "fwav_debug_topk_geometry: outside [-1, 1]");
+  FWAV_CHECK_ARG(wide >= -1 && wide <= 2, FWAV_ERR_ARG, "fwav_debug_topk_geometry: outside [-1, 2]");
   g_wide = wide;
   return FWAV_OK;
 }
@@ -1979,9 +2220,12 @@ int fwav_debug_topk_geometry(int wide) {
 // A query of a whole-table block or a query half must be counted once, one of a block split into P table pieces P
 // times.  *items = the launch's grid.
 int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t* count, int64_t* items) {
-  FWAV_CHECK_ARG(n >= 0 && count && items && (pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces)), FWAV_ERR_ARG,
+  FWAV_CHECK_ARG(n >= 0 && count && items && wide >= 0 && wide <= 2 &&
+                     (pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces)), FWAV_ERR_ARG,
                  "fwav_debug_topk_plan_cover: bad args");
-  const int W = wide ? kWideW : k16Waves, qb = 32 * W * k16Sets;
+  const int geo = wide;  // 0 base, 1 wide, 2 centroid
+  const int W = geo == kGeoWide ? kWideW : (geo == kGeoCent ? kCentW : k16Waves);
+  const int sets = geo == kGeoCent ? kCentQS : k16Sets, qb = 32 * W * sets;
   const TopkPlan pl = make_plan(n, rt, pieces, qb);
   *items = pl.items();
   for (int64_t it = 0; it < pl.items(); ++it) {
@@ -1990,8 +2234,8 @@ int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t*
     plan_item(pl, it, block, piece, np, qhalf);
     if (block >= pl.nb) continue;
     const int wact = qhalf < 0 ? W : W / 2;
-    const int qslot0 = qhalf > 0 ? (W / 2) * k16Sets * 32 : 0;
-    for (int ql = 0; ql < wact * k16Sets * 32; ++ql) {
+    const int qslot0 = qhalf > 0 ? (W / 2) * sets * 32 : 0;
+    for (int ql = 0; ql < wact * sets * 32; ++ql) {
       const int64_t qi = slot_query(block, qslot0 + ql, pl.nb, qb);
       if (qi < n) ++count[qi];
     }
@@ -2004,11 +2248,11 @@ int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t*
 // halves), grid.
 int fwav_debug_topk_plan_info(int64_t max_q, int64_t nd, int32_t* info, int64_t* blocks) {
   FWAV_CHECK_ARG(max_q >= 0 && nd > 0 && info && blocks, FWAV_ERR_ARG, "fwav_debug_topk_plan_info: bad args");
-  const bool wide = wide_geometry(nd);
+  const int geo = first_geometry(nd);
   int rt, P;
-  host_plan_for(max_q, nd, wide, rt, P);
-  const TopkPlan pl = make_plan(max_q, rt, P, wide ? kWideQB : k16QB);
-  info[0] = wide ? 1 : 0;
+  host_plan_for(max_q, nd, geo, rt, P);
+  const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(geo));
+  info[0] = geo;
   info[1] = first_mode(nd);
   info[2] = pl.halves ? -1 : pl.P;
   blocks[0] = pl.F;

@@ -23,15 +23,13 @@ import numpy as np
 import torch
 
 from . import _lib, ties as _ties
+from .nporder import zero_query_candidates  # noqa: F401  (Q11 rows; re-exported)
 from ._lib import FwavError, call, size_call
 
 F32 = np.float32
 
 
-def geometry(tile_size: int) -> tuple[int, int]:
-    """range_size, domain_step (fractal.py:1070-1071)."""
-    rs = max(4, tile_size // 256)
-    return rs, max(1, rs // 4)
+from . import geometry  # noqa: E402,F401  range_size, domain_step (fractal.py:1070-1071)
 
 
 def n_domains_for(n: int, tile_size: int, step: int) -> int:
@@ -63,30 +61,6 @@ def embed_tables(rs: int, device: torch.device) -> torch.Tensor:
         call("fwav_embed_tables", rs, host.ctypes.data)
         _TABLES[key] = torch.from_numpy(host).to(device)
     return _TABLES[key]
-
-
-_ZERO_CAND: dict = {}
-
-
-def zero_query_candidates(n_domains: int, top_k: int) -> np.ndarray:
-    """The reference's candidate row for a query whose embedding is all zero (quirk Q11): every score is 0, so the row
-    is the order in which numpy's introselect (``argpartition``) and ``argsort`` leave equal keys —
-    ``range_candidates_from_embedding_emb`` (fractal.py:535-541) evaluated on a zero score vector, padded with −1 by
-    ``pad_candidates`` (fractal.py:544-552).  A K-element constant per (n_domains, K), computed once on the host by
-    the same numpy calls the reference makes (the tie order is numpy's, so it is taken from numpy)."""
-    key = (int(n_domains), int(top_k))
-    if key not in _ZERO_CAND:
-        nd, k = key
-        scores = np.zeros(nd, np.float32)
-        if k >= nd:
-            idx = np.argsort(scores)[::-1].astype(np.int32)
-        else:
-            part = np.argpartition(scores, -k)[-k:]
-            idx = part[np.argsort(scores[part])[::-1]].astype(np.int32)
-        out = np.full(k, -1, np.int32)
-        out[:min(k, len(idx))] = idx[:k]
-        _ZERO_CAND[key] = out
-    return _ZERO_CAND[key]
 
 
 _ZERO_CAND_DEV: dict = {}

@@ -124,6 +124,9 @@ def affine_hbm_roofline(dev, K: int, n_queries: int = 262_144, reps: int = 10) -
                                "note": f"{n_rows} uniformly random {4 * rs}-B rows of the same pool, cold, nothing "
                                        f"computed (fwav_debug_gather_rows)"},
             "rows_per_s": n_rows / (ms_cold * 1e-3),
+            # the north star's ≥ 60 % HBM stated against what random 32-B rows allow on this chip: the solve's row rate
+            # over the gather-only ceiling's (> 1: candidate rows cluster, so the L2 dedups neighbouring ranges' rows)
+            "frac_of_gather_ceiling": ms_gather / ms_cold,
             "equals_pipeline_output": same,
             "workload": f"cfg4 (60 min 48 kHz noise): the real top-{K} candidates of its first {q} ranges, pool of "
                         f"{nd} rows ({nd * rs * 4 / 1e9:.2f} GB, above the 256 MB MALL)"}

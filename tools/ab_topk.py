@@ -57,12 +57,17 @@ wsn = 0
 for _, L in libs:
     L.fwav_sim_topk_workspace_size.restype = C.c_size_t
     L.fwav_sim_topk_workspace_size.argtypes = [C.c_int64, C.c_int64, C.c_int]
+    if os.environ.get("AB_PLAN"):
+        L.fwav_debug_topk_plan(*[int(x) for x in os.environ["AB_PLAN"].split(",")])
     wsn = max(wsn, L.fwav_sim_topk_workspace_size(nq, nd, 64))
 wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
 outs = {}
 times = {n: [] for n, _ in libs}
+plan = os.environ.get("AB_PLAN")  # "rt,pieces": the work-plan override of every build (fwav_debug_topk_plan)
 for rnd in range(int(os.environ.get("AB_ROUNDS", 4))):
     for name, L in libs:
+        if plan:
+            L.fwav_debug_topk_plan(*[int(x) for x in plan.split(",")])
         cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
@@ -78,6 +83,11 @@ for rnd in range(int(os.environ.get("AB_ROUNDS", 4))):
             times[name].append(e0.elapsed_time(e1))
         # only the searched rows are written (rows past nq, or the pruned ranges' rows of the engine's active list)
         outs[name] = cand[:nq * 64] if cfg in ("cfg2", "cfg4") else cand.view(-1, 64)[active.long()]
+        if rnd == 0 and hasattr(L, "fwav_debug_cent_stats"):
+            cs = (C.c_ulonglong * 4)()
+            L.fwav_debug_cent_stats(cs)
+            print(f"{name:24s} centroid filter: {cs[0]} level-1 tiles, {cs[1]} level-2 (tile, set) pairs "
+                  f"({cs[1] / max(cs[0], 1):.3f} per tile)", flush=True)
         if rnd == 0:  # overflowed queries of this build: the i32 count at the end of its own workspace layout
             own = L.fwav_sim_topk_workspace_size(nq, nd, 64)
             o = own - 4 - 4 * max(nq, 1)  # ovf list, count, then u32 seeds[q]
