@@ -378,7 +378,11 @@ constexpr int kModeS16 = 0, kModeHL = 1, kModeEX = 2;
 #define FWAV_TOPK_FIRST -1
 #endif
 constexpr int64_t kHLFirstMinDomains = int64_t(1) << 22;
-static int g_first_mode = -1;  // fwav_debug_topk_mode (tests): force S16 / HL
+#ifdef FWAV_DEBUG_API
+static int g_first_mode = -1;  // fwav_debug_topk_mode (debug library only): force S16 / HL
+#else
+constexpr int g_first_mode = -1;  // the product library has no process-global knobs
+#endif
 __host__ inline int first_mode(int64_t nd) {
   if (g_first_mode >= 0) return g_first_mode;
   return FWAV_TOPK_FIRST >= 0 ? FWAV_TOPK_FIRST : (nd > kHLFirstMinDomains ? kModeHL : kModeS16);
@@ -419,6 +423,13 @@ __device__ __forceinline__ void stat_add_p(unsigned long long* stats, int i, uns
 }
 extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #define stat_add(i, v) stat_add_p(stats, (i), (v))
+// Experiment code paths exist only in the debug library (libfwav_debug.so, -DFWAV_DEBUG_API; tools/ab_build.sh):
+// the product library never carries them.
+#if !defined(FWAV_DEBUG_API) && (defined(FWAV_TOPK_EXTSEED) || defined(FWAV_TOPK_DEBUG) || \
+                                 defined(FWAV_TOPK_ABL) || defined(FWAV_TOPK_CENTSTATS) || \
+                                 defined(FWAV_TOPK_CENT_L2OFF) || defined(FWAV_TOPK_PADLDS))
+#error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
+#endif
 // Production geometry (the -D overrides build A/B variants: tools/ab_topk.py)
 #ifndef FWAV_TOPK_G
 #define FWAV_TOPK_G 4
@@ -445,6 +456,9 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #endif
 #ifndef FWAV_TOPK_CWPE
 #define FWAV_TOPK_CWPE 2
+#endif
+#ifndef FWAV_TOPK_CB
+#define FWAV_TOPK_CB 2  // centroid level 2: (tile, set) pairs in flight together
 #endif
 // Ablation builds (tools/ab_build.sh NAME -DFWAV_TOPK_ABL=<dbg bits>): the production kernel with the given `dbg`
 // bits fixed at compile time — the STATS kernel's counters cost registers (it spills), which skews its timings.
@@ -1256,6 +1270,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 // — a 4:1 (QS = 4) reduction of the fold, the stream's issue bound — decides which sets need their own MFMA and fold
 // for that tile: a set is scored only where some centroid of it reaches the smallest member threshold minus the
 // centroid's slack.  Exact: a tile skipped for a set holds no domain above any member's threshold.
+constexpr int kCentBatch = FWAV_TOPK_CB;
 #ifdef FWAV_TOPK_CENTSTATS
 __device__ unsigned long long g_cent_stats[4];  // experiment builds: level-1 tiles, level-2 (tile, set) pairs
 #endif
@@ -1592,25 +1607,48 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           for (int s = 0; s < QS; ++s) pend[s] |= pc[s] << (8 * (c - cg));
         }
       }
-      // level 2: each marked (tile, set) scored with the set's queries; survivors appended now (the tile is in LDS)
+      // level 2: the marked (tile, set) pairs scored with the set's queries, kCentBatch at a time (their fragments and
+      // MFMAs in flight together; HL: the low-part fragments fetched from L2 with them), survivors appended now
       static_for<QS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
         uint64_t pm = pend[s];
         while (pm != 0ull) {
-          const int t = __builtin_ctzll(pm);
-          pm &= pm - 1;
-          const half8 af = *reinterpret_cast<const half8*>(lda0 + (t >> 3) * (512 * 8) + (t & 7) * 256);
-          floatx16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, b[s], floatx16{}, 0, 0, 0);
-          const int64_t dt = (int64_t)(cg + (t >> 3)) * kChunk + (t & 7) * 32;
-          if constexpr (HL) {  // shl = s16 + d_hi·q_lo + d_lo·q_hi, refined only where some s16 can pass
-            if (__ballot(fold16((int)0x80000000, acc) > thi[s]) == 0ull) continue;
-            const half8 afl = tile_fragment(emb16lo, dt, h, col);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl, b[s], acc, 0, 0, 0);
+          int t[kCentBatch];
+          bool on[kCentBatch];
+#pragma unroll
+          for (int u = 0; u < kCentBatch; ++u) {
+            on[u] = pm != 0ull;
+            t[u] = on[u] ? __builtin_ctzll(pm) : t[0];
+            if (on[u]) pm &= pm - 1;
           }
-          thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(acc, thf[s], qcnt[s], kept[s], dt, nd,
-                                                                             gkeys, sm, wave * QS + s, K, upd[s],
-                                                                             stats, sp, emb, qv[s], &kth[s], share);
+          half8 af[kCentBatch], afl[HL ? kCentBatch : 1];
+          floatx16 acc[kCentBatch];
+#pragma unroll
+          for (int u = 0; u < kCentBatch; ++u)
+            af[u] = *reinterpret_cast<const half8*>(lda0 + (t[u] >> 3) * (512 * 8) + (t[u] & 7) * 256);
+          if constexpr (HL) {
+#pragma unroll
+            for (int u = 0; u < kCentBatch; ++u)
+              afl[u] = tile_fragment(emb16lo, (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32, h, col);
+          }
+#pragma unroll
+          for (int u = 0; u < kCentBatch; ++u)
+            acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], b[s], floatx16{}, 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < kCentBatch; ++u) {
+            if (!on[u]) break;
+            const int64_t dt = (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32;
+            floatx16 a2 = acc[u];
+            if constexpr (HL) {  // shl = s16 + d_hi·q_lo + d_lo·q_hi, refined only where some s16 can pass
+              if (__ballot(fold16((int)0x80000000, a2) > thi[s]) == 0ull) continue;
+              a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], bl[s], a2, 0, 0, 0);
+              a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl[u], b[s], a2, 0, 0, 0);
+            }
+            thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(a2, thf[s], qcnt[s], kept[s], dt,
+                                                                               nd, gkeys, sm, wave * QS + s, K,
+                                                                               upd[s], stats, sp, emb, qv[s],
+                                                                               &kth[s], share);
+          }
         }
       });
     } else if (ABL && (dbg & (512 | 1024)) && c_end - cg == G) {
@@ -1843,7 +1881,11 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
 }
 
 // Host-side plan: default policy from the device's workgroup slots, or a diagnostic override.
-static int g_plan_rt = -1, g_plan_p = -1;
+#ifdef FWAV_DEBUG_API
+static int g_plan_rt = -1, g_plan_p = -1;  // fwav_debug_topk_plan (debug library only)
+#else
+constexpr int g_plan_rt = -1, g_plan_p = -1;
+#endif
 // Per-device caches (the caller makes the stream's device current: fwav.engine wraps every call in
 // torch.cuda.device); kMaxDev bounds the device ordinal.
 constexpr int kMaxDev = 64;
@@ -1867,7 +1909,11 @@ constexpr int kWideW = 16, kWideG = 8;
 constexpr int kWideQB = 32 * kWideW;
 constexpr int kCentQS = FWAV_TOPK_CENT > 0 ? FWAV_TOPK_CENT : 4, kCentW = FWAV_TOPK_CW, kCentG = FWAV_TOPK_CG;
 constexpr int kCentQB = 32 * kCentW * kCentQS;
-static int g_wide = -1;  // fwav_debug_topk_geometry (tests): force base / wide / centroid
+#ifdef FWAV_DEBUG_API
+static int g_wide = -1;  // fwav_debug_topk_geometry (debug library only): force base / wide / centroid
+#else
+constexpr int g_wide = -1;
+#endif
 // first-pass geometries
 constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2;
 static int first_geometry(int64_t nd) {
@@ -2010,7 +2056,12 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     (void)hipMemsetAsync(n_ovf2, 0, sizeof(int32_t), st);
     // Geometry: k16Waves waves × k16Sets query sets of 32 per workgroup.  Measured at cfg2 (W, QS=1): W = 8
     // 27.9 ms, W = 7 31.6 ms, W = 6 44.5 ms — an even 4 waves per SIMD beats a fuller last round of workgroups.
+#ifdef FWAV_DEBUG_API
     const bool stats_first = (stats != nullptr && !(dbg & (1 << 17))) || (dbg & 65535) != 0;
+#else
+    constexpr bool stats_first = false;  // counter / ablation launches: debug library only
+    (void)dbg;
+#endif
     // counter (STATS) builds of the first pass exist in the base geometry only
     const int geo = stats_first ? kGeoBase : first_geometry(nd);
     const bool wide = geo == kGeoWide;
@@ -2039,10 +2090,13 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
     } else
 #endif
+#ifdef FWAV_DEBUG_API
     if (stats_first) {
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, true, dbg & 65535, stats);
       else FWAV_FIRST(kModeS16, true, dbg & 65535, stats);
-    } else if (wide) {
+    } else
+#endif
+    if (wide) {
       if (mode1 == kModeHL) FWAV_FIRST_WIDE(kModeHL); else FWAV_FIRST_WIDE(kModeS16);
     } else if (geo == kGeoCent) {
       if (mode1 == kModeHL) FWAV_FIRST_CENT(kModeHL); else FWAV_FIRST_CENT(kModeS16);
@@ -2081,11 +2135,13 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       ex_n = n_ovf2;
       ex_seeds = seeds2;
     }
+#ifdef FWAV_DEBUG_API
     if (stats != nullptr && (dbg & (1 << 17)))  // diagnostic: counters of the exact-mode relaunch only
       k_sim_topk_f16<k16Cap, true, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, ex_seeds, kStreamMargin, 0, 1, 0,
           stats, sp, ties);
     else
+#endif
       k_sim_topk_f16<k16Cap, false, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, ex_seeds, kStreamMargin, 0, 1, 0,
           nullptr, sp, ties);
@@ -2168,6 +2224,7 @@ int fwav_score_rows(const float* emb, int64_t nd, const int32_t* rows, int64_t n
                            (hipStream_t)stream);
 }
 
+#ifdef FWAV_DEBUG_API  // ---- debug library only (include/fwav_debug.h)
 // Diagnostic ablations of the fp16 search kernel (timing only; see k_sim_topk_f16 `dbg`).
 int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t nd, const int32_t* active, const int32_t* n_active,
                         int64_t max_q, int64_t q_offset, int K, int32_t* cand, void* workspace, size_t ws_bytes, int dbg,
@@ -2270,5 +2327,7 @@ int fwav_debug_topk_plan(int rt, int pieces) {
   g_plan_p = rt < 0 ? -1 : pieces;
   return FWAV_OK;
 }
+
+#endif  // FWAV_DEBUG_API
 
 }  // extern "C"

@@ -12,6 +12,7 @@ from . import _digest
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfwav.so")
+DEBUG_LIB_PATH = os.path.join(_HERE, "libfwav_debug.so")
 
 P = C.c_void_p
 I64 = C.c_int64
@@ -42,11 +43,6 @@ SIGNATURES = {
     "fwav_sim_topk_workspace_size": (SZ, [I64, I64, I32]),
     "fwav_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, I32, P, P, P, SZ, P]),
     "fwav_score_rows": (I32, [P, I64, P, I64, I64, I32, P, P]),
-    "fwav_debug_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, SZ, I32, P, P]),
-    "fwav_debug_topk_plan": (I32, [I32, I32]),
-    "fwav_debug_topk_plan_cover": (I32, [I64, I32, I32, I32, P, P]),
-    "fwav_debug_topk_mode": (I32, [I32]),
-    "fwav_debug_topk_geometry": (I32, [I32]),
     "fwav_debug_gather_rows": (I32, [P, I64, I32, I64, P, P]),
     "fwav_affine": (I32, [P, I64, I32, P, I32, P, I64, F32, P, P, P, P, P, P]),
     "fwav_tie_check": (I32, [P, I64, I32, P, I32, P, I64, P, I64, I32, P, I64, I32, P, P]),
@@ -54,7 +50,6 @@ SIGNATURES = {
     "fwav_tie_rows_out": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P]),
     "fwav_tie_list_size": (I64, [I64]),
     "fwav_emb16_from_emb": (I32, [P, I64, P, P]),
-    "fwav_debug_topk_plan_info": (I32, [I64, I64, P, P]),
     "fwav_decode_workspace_size": (SZ, [I64, I32, I32]),
     "fwav_decode": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, SZ, P]),
     "fwav_decode_span": (I32, []),
@@ -66,38 +61,88 @@ SIGNATURES = {
     "fwav_decode_finish": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P]),
 }
 
+#: the debug library's extra entry points (include/fwav_debug.h): the search's process-global test knobs and
+#: diagnostics; libfwav.so exports none of them
+DEBUG_SIGNATURES = {
+    "fwav_debug_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, SZ, I32, P, P]),
+    "fwav_debug_topk_plan": (I32, [I32, I32]),
+    "fwav_debug_topk_plan_cover": (I32, [I64, I32, I32, I32, P, P]),
+    "fwav_debug_topk_mode": (I32, [I32]),
+    "fwav_debug_topk_geometry": (I32, [I32]),
+    "fwav_debug_topk_plan_info": (I32, [I64, I64, P, P]),
+}
+
 
 class FwavError(RuntimeError):
     """A C-ABI call returned a non-zero status (message from ``fwav_last_error``)."""
 
 
-_lib = None
+_libs: dict = {}
+_active = None  # the debug library inside debug_library(), else the product library
+
+
+def _load(path: str, sigs: dict) -> C.CDLL:
+    if not os.path.exists(path):
+        raise FwavError(f"HIP library not built: {path} is missing (run __graft_entry__.build())")
+    dll = C.CDLL(path)
+    dll.fwav_build_digest.restype = C.c_char_p
+    built = dll.fwav_build_digest().decode()
+    want = _digest.source_digest()
+    if want is not None and built != want:
+        raise FwavError(f"{path} was built from other sources (digest {built[:12]}, sources {want[:12]}): "
+                        "run __graft_entry__.build()")
+    for name, (res, args) in sigs.items():
+        fn = getattr(dll, name)
+        fn.restype = res
+        fn.argtypes = args
+    return dll
+
+
+def product_lib() -> C.CDLL:
+    """libfwav.so, the product library (include/fwav.h)."""
+    if "product" not in _libs:
+        _libs["product"] = _load(LIB_PATH, SIGNATURES)
+    return _libs["product"]
+
+
+def debug_lib() -> C.CDLL:
+    """libfwav_debug.so (include/fwav_debug.h): the same entry points plus the search's test knobs; tests only."""
+    if "debug" not in _libs:
+        _libs["debug"] = _load(DEBUG_LIB_PATH, {**SIGNATURES, **DEBUG_SIGNATURES})
+    return _libs["debug"]
 
 
 def lib() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise FwavError(f"HIP library not built: {LIB_PATH} is missing (run __graft_entry__.build())")
-        dll = C.CDLL(LIB_PATH)
-        dll.fwav_build_digest.restype = C.c_char_p
-        built = dll.fwav_build_digest().decode()
-        want = _digest.source_digest()
-        if want is not None and built != want:
-            raise FwavError(f"{LIB_PATH} was built from other sources (digest {built[:12]}, sources {want[:12]}): "
-                            "run __graft_entry__.build()")
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(dll, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = dll
-    return _lib
+    """The library every fwav call goes through: the product library, or the debug one inside debug_library()."""
+    return _active if _active is not None else product_lib()
+
+
+class debug_library:
+    """``with debug_library(): ...`` routes every fwav call of the block (fwav.engine included) through
+    libfwav_debug.so, whose process-global knobs (fwav_debug_topk_plan / _mode / _geometry) the block may set; they
+    are reset to the defaults on exit.  Test-only: not thread-safe, not re-entrant across threads."""
+
+    def __enter__(self):
+        global _active
+        self.prev = _active
+        _active = debug_lib()
+        return _active
+
+    def __exit__(self, *exc):
+        global _active
+        d = debug_lib()
+        d.fwav_debug_topk_plan(-1, 1)
+        d.fwav_debug_topk_mode(-1)
+        d.fwav_debug_topk_geometry(-1)
+        _active = self.prev
+        return False
 
 
 def call(name: str, *args) -> int:
-    rc = getattr(lib(), name)(*args)
+    L = lib()
+    rc = getattr(L, name)(*args)
     if rc != 0:
-        msg = lib().fwav_last_error().decode(errors="replace")
+        msg = L.fwav_last_error().decode(errors="replace")
         raise FwavError(f"{name} failed ({rc}): {msg}")
     return rc
 

@@ -13,6 +13,8 @@
  *     No exception, abort or exit crosses the ABI.
  *   - Workspaces are caller-allocated; *_workspace_size() gives the byte count.
  *   - Results are deterministic for identical inputs.
+ *   - No entry point reads or writes process-global state: the test and experiment knobs of the search live in the
+ *     separate debug library (libfwav_debug.so, include/fwav_debug.h).
  */
 #ifndef FWAV_H
 #define FWAV_H
@@ -122,39 +124,6 @@ int fwav_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const 
  * Replaces `scores = domain_embs @ q` (fractal.py:537). */
 int fwav_score_rows(const float* emb, int64_t n_domains, const int32_t* rows, int64_t n_rows, int64_t q_offset,
                     int blas_threads, float* scores, void* stream);
-/* Diagnostic ablations of the fp16 kernel (timing only, outputs invalid for dbg & 65535 != 0); stats (u64[16]
- * device, may be NULL) receives slow-path counters — of the first pass, or with dbg = 1 << 17 of the exact-mode
- * relaunch for overflowed queries only (outputs valid).  Not used by the product path. */
-int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
-                        const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand,
-                        void* workspace, size_t ws_bytes, int dbg, unsigned long long* stats, void* stream);
-/* The three overrides below (fwav_debug_topk_plan / _mode / _geometry) are PROCESS-GLOBAL test knobs, not thread-safe:
- * they change which kernels fwav_sim_topk launches and how much workspace it needs, so set them only while no search
- * is being sized or is in flight on any thread, and re-query fwav_sim_topk_workspace_size after a change (a search
- * sized before the change is rejected with FWAV_ERR_WORKSPACE when it needs more).  The product never sets them.
- *
- * Diagnostic override of the fp16 search's work plan: the last `rt` query blocks are split into `pieces` table
- * ranges, or with pieces == -1 into two query halves (rt < 0 restores the default policy).  Every plan returns the
- * same candidates.  Re-query fwav_sim_topk_workspace_size afterwards. */
-int fwav_debug_topk_plan(int rt, int pieces);
-/* The first pass fwav_sim_topk would launch for max_q queries over n_domains domains on the current device (host
- * only): info[0] = geometry (1 = wide), info[1] = first-pass mode (0 = fp16 band, 1 = hi/lo band), info[2] = table
- * pieces per split block (−1: query halves); blocks[0] = whole-table blocks, blocks[1] = split blocks,
- * blocks[2] = grid. */
-int fwav_debug_topk_plan_info(int64_t max_q, int64_t n_domains, int32_t* info, int64_t* blocks);
-/* Host-side check of a work plan (no device): count[position] += 1 for every query slot of every item of the plan of
- * n queries (whole blocks and query halves cover a query once, a block in P table pieces P times); *items = grid. */
-int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t* count, int64_t* items);
-/* Diagnostic override of the fp16 search's first-pass mode: 0 = fp16 band (overflowing queries relaunched with the
- * hi/lo band, then exact keys), 1 = hi/lo band (then exact keys), −1 = by table size (the default: hi/lo above 4 Mi
- * domains).  Every mode returns the same candidates. */
-int fwav_debug_topk_mode(int mode);
-/* Diagnostic override of the fp16 search's first-pass geometry: 0 = 8 waves × 32 queries per workgroup, 1 = 16 waves
- * × 32 queries, one workgroup per CU (the table streamed once per 512 queries), −1 = by table size (the default: wide
- * above 8 Mi domains, where the table outgrows the Infinity Cache).  Both return the same candidates.  Re-query
- * fwav_sim_topk_workspace_size afterwards. */
-int fwav_debug_topk_geometry(int wide);
-
 /* ------------------------------------------------------------------- batched affine solve
  * Replaces _flush_gpu_batch / _process_gpu_batch (fractal.py:852-870, 757-850): per range, over the K
  * candidates and their mirrors, s = Σd̃r̃/(Σd̃²+1e-12), o = r̄ − s·d̄, err = ‖s·D+o−R‖₂ (+inf for cand < 0),

@@ -1,5 +1,6 @@
 """The C-ABI library: loads on CPU, exports exactly what include/fwav.h declares, binds with the right arity,
-rejects bad arguments with status codes (no GPU needed: argument checks run before any HIP call)."""
+rejects bad arguments with status codes (no GPU needed: argument checks run before any HIP call).  The debug library
+(libfwav_debug.so, include/fwav_debug.h) adds the search's test knobs; the product library exports none of them."""
 import ctypes
 import os
 import re
@@ -9,10 +10,11 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "fwav.h")
+DEBUG_HEADER = os.path.join(ROOT, "include", "fwav_debug.h")
 
 
-def header_functions():
-    txt = open(HEADER).read()
+def header_functions(path=HEADER):
+    txt = open(path).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     out = {}
     for m in re.finditer(r"^\s*(?:const\s+)?[\w]+\s*\*?\s*(fwav_\w+)\s*\(([^;]*?)\);", txt, flags=re.M | re.S):
@@ -42,6 +44,27 @@ def test_bindings_match_header(lib):
     assert set(decl) == set(lib.SIGNATURES), set(decl) ^ set(lib.SIGNATURES)
     for name, n in decl.items():
         assert len(lib.SIGNATURES[name][1]) == n, name
+
+
+def test_debug_library_split(lib):
+    """include/fwav_debug.h declares exactly the debug bindings; libfwav_debug.so exports them and every product entry
+    point, libfwav.so none of them (no process-global knob in the product library)."""
+    decl = header_functions(DEBUG_HEADER)
+    assert set(decl) == set(lib.DEBUG_SIGNATURES), set(decl) ^ set(lib.DEBUG_SIGNATURES)
+    for name, n in decl.items():
+        assert len(lib.DEBUG_SIGNATURES[name][1]) == n, name
+    prod = ctypes.CDLL(lib.LIB_PATH)
+    dbg = ctypes.CDLL(lib.DEBUG_LIB_PATH)
+    for name in decl:
+        assert hasattr(dbg, name) and not hasattr(prod, name), name
+    for name in header_functions():
+        assert hasattr(dbg, name), name
+    assert lib.debug_lib().fwav_build_digest() == lib.product_lib().fwav_build_digest()
+    # the knobs are reachable only through debug_library(), which resets them on exit
+    with lib.debug_library() as d:
+        assert lib.lib() is d
+        lib.call("fwav_debug_topk_geometry", 0)
+    assert lib.lib() is lib.product_lib()
 
 
 def test_error_codes_without_gpu(lib):
@@ -80,14 +103,15 @@ def test_debug_search_rejects_workspace_of_another_query_count(lib):
     """Round 2's memory fault (tools/phase_ab.py): a workspace sized for 41,344 queries was handed to a search of
     20,672, whose table-pieces plan needs more key buffers.  The debug entry point now takes the workspace size and
     rejects a short one before any launch; the product always sizes for the query count it launches."""
-    L = lib.lib()
+    L = lib.debug_lib()
     nd = 1_321_977
     sizes = {q: L.fwav_sim_topk_workspace_size(q, nd, 64) for q in (20672, 41344, 65536, 82688, 131072)}
     # a workspace sized for more queries can be too small for fewer (their plan splits more blocks into pieces)
+    # (the sizes also cover the centroid geometry's plans, which can make them monotonic in the query count)
     pairs = [(a, b) for a in sizes for b in sizes if b < a and sizes[b] > sizes[a]]
-    assert pairs, sizes
     p = ctypes.c_void_p(16)
-    for q, ws in [(pairs[0][1], sizes[pairs[0][0]]), (20672, sizes[20672] - 1)]:
+    cases = [(pairs[0][1], sizes[pairs[0][0]])] if pairs else []
+    for q, ws in cases + [(20672, sizes[20672] - 1), (41344, sizes[20672])]:
         rc = L.fwav_debug_sim_topk(p, p, nd, p, p, q, 0, 64, p, p, ws, 0, None, None)
         assert rc == -5 and b"workspace" in L.fwav_last_error(), (q, ws)
 
@@ -156,7 +180,8 @@ def test_work_plan_covers_every_query(lib, n, rt, pieces, wide):
     runs every active query exactly once per table piece of its block and nothing past the list."""
     count = np.zeros(n, np.int32)
     items = ctypes.c_int64()
-    lib.call("fwav_debug_topk_plan_cover", n, rt, pieces, wide, count.ctypes.data, ctypes.addressof(items))
+    with lib.debug_library():
+        lib.call("fwav_debug_topk_plan_cover", n, rt, pieces, wide, count.ctypes.data, ctypes.addressof(items))
     qb = 32 * (16 if wide else 8)
     nb = -(-n // qb)
     P = 1 if pieces == 1 else (2 if pieces == -1 else pieces)

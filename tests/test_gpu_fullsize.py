@@ -18,7 +18,7 @@ import pytest
 torch = pytest.importorskip("torch")
 
 from fwav import engine, synth, ties  # noqa: E402
-from fwav._lib import call, size_call  # noqa: E402
+from fwav._lib import call, debug_library, size_call  # noqa: E402
 from oracle import fractal_oracle as O  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -255,18 +255,17 @@ def test_cfg4_shard_wide_geometry_default():
     nd = res.n_domains
     info = np.zeros(3, np.int32)
     blocks = np.zeros(3, np.int64)
-    call("fwav_debug_topk_plan_info", q, nd, info.ctypes.data, blocks.ctypes.data)
+    with debug_library():
+        call("fwav_debug_topk_plan_info", q, nd, info.ctypes.data, blocks.ctypes.data)
     print(f"cfg4 shard plan: wide {info[0]} mode {info[1]} pieces {info[2]} whole blocks {blocks[0]} split "
           f"{blocks[1]} grid {blocks[2]}")
     assert info[0] == 1 and blocks[0] > 0 and blocks[0] * 512 >= q // 2
     wide = res.cand.view(-1, K).cpu().numpy()
     assert (wide >= 0).all() and (wide < nd).all()
-    call("fwav_debug_topk_geometry", 0)
-    try:
+    with debug_library():
+        call("fwav_debug_topk_geometry", 0)
         base = engine.compress_device(x, 2048, K, shard=(0, q), keep_intermediates=True, tie_order="index")
         torch.cuda.synchronize()
-    finally:
-        call("fwav_debug_topk_geometry", -1)
     assert np.array_equal(wide, base.cand.view(-1, K).cpu().numpy())
     rows = np.arange(0, q, q // 1024)[:1024]
     assert np.array_equal(wide[rows], f32_search(res, rows, K))

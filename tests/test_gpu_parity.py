@@ -14,7 +14,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from fwav import engine  # noqa: E402
-from fwav._lib import call  # noqa: E402
+from fwav._lib import call, debug_library  # noqa: E402
 
 
 def dev():
@@ -156,11 +156,10 @@ def first_mode(request):
     """Run a test under each first-pass mode (fwav_debug_topk_mode) and workgroup geometry (fwav_debug_topk_geometry)
     of the fp16 search, then restore the defaults."""
     mode, wide = request.param
-    call("fwav_debug_topk_mode", mode)
-    call("fwav_debug_topk_geometry", wide)
-    yield mode
-    call("fwav_debug_topk_mode", -1)
-    call("fwav_debug_topk_geometry", -1)
+    with debug_library():  # the knobs exist in libfwav_debug.so only; the whole test runs through it
+        call("fwav_debug_topk_mode", mode)
+        call("fwav_debug_topk_geometry", wide)
+        yield mode
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -257,14 +256,11 @@ def test_f16_split_plans_equal_f32(plan, wide):
     from fwav import synth
     sig = synth.noise(6.0, 44100, seed=11)
     b, _ = _cands(sig, 2048, 64, "f32")
-    call("fwav_debug_topk_plan", *plan)
-    call("fwav_debug_topk_geometry", wide)
-    try:
+    with debug_library():
+        call("fwav_debug_topk_plan", *plan)
+        call("fwav_debug_topk_geometry", wide)
         a, _ = _cands(sig, 2048, 64, "f16")
         p, _ = _cands(_periodic(), 1024, 32, "f16")  # band overflow inside pieces → exact-mode relaunch after the merge
-    finally:
-        call("fwav_debug_topk_plan", -1, 1)
-        call("fwav_debug_topk_geometry", -1)
     assert np.array_equal(a, b)
     q, _ = _cands(_periodic(), 1024, 32, "f32")
     assert np.array_equal(p, q)

@@ -7,9 +7,9 @@ import os
 def use(path: str) -> None:
     from fwav import _lib
     dll = C.CDLL(os.path.abspath(path))
-    for name, (res, args) in _lib.SIGNATURES.items():
+    for name, (res, args) in {**_lib.SIGNATURES, **_lib.DEBUG_SIGNATURES}.items():
         fn = getattr(dll, name, None)
         if fn is not None:
             fn.restype, fn.argtypes = res, args
     _lib.LIB_PATH = os.path.abspath(path)
-    _lib._lib = dll
+    _lib._libs["product"] = _lib._libs["debug"] = dll

@@ -7,7 +7,7 @@ name=$1
 shift
 out=tools/ab/obj_$name
 mkdir -p "$out"
-flags=(--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt "$@")
+flags=(--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -DFWAV_DEBUG_API "$@")
 pids=()
 for s in audio-compression_amd/csrc/*.hip; do
   hipcc "${flags[@]}" -c "$s" -o "$out/$(basename "$s" .hip).o" &
