@@ -98,6 +98,7 @@ class DeviceCompressed:
     n_active: Optional[torch.Tensor] = None
     energy_partial: Optional[torch.Tensor] = None
     ties: Optional[torch.Tensor] = None  # fwav_sim_topk's tie list (keep_intermediates)
+    resolved: Optional[torch.Tensor] = None  # local rows re-ranked with numpy's order (keep_intermediates)
     n_ties: int = 0          # queries whose top K + 1 scores hold exact ties
     n_resolved: int = 0      # of those, rows re-ranked with numpy's own tie order (fwav.ties)
     empty: bool = False
@@ -341,6 +342,8 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
                 res.pending = _ties.defer(stage, dev)
             else:
                 finish(st)
+                if keep_intermediates:
+                    res.resolved = resolve[1:1 + res.n_resolved]
             _mark(events, "ties")
         elif sliced:
             ties = _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb16, active, n_active,
@@ -436,6 +439,7 @@ def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb1
                              cand=cand, outs=outs, stream=_stream(dev))
 
     res.n_ties, res.n_resolved = n_ties, n_res
+    res.resolved = torch.cat([r for r, _ in pend]) if pend else torch.empty(0, dtype=torch.int32, device=dev)
     if defer:  # wait() applies the rankings on the caller's stream
         res.pending, res.apply = _Staged(pend), apply
     else:
