@@ -460,6 +460,9 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_CB
 #define FWAV_TOPK_CB 2  // centroid level 2: (tile, set) pairs in flight together
 #endif
+#ifndef FWAV_TOPK_CSHARE
+#define FWAV_TOPK_CSHARE 1  // centroid geometry: read the pieces' shared limits every group (else at window ends)
+#endif
 // Ablation builds (tools/ab_build.sh NAME -DFWAV_TOPK_ABL=<dbg bits>): the production kernel with the given `dbg`
 // bits fixed at compile time — the STATS kernel's counters cost registers (it spills), which skews its timings.
 #ifndef FWAV_TOPK_ABL
@@ -1585,6 +1588,14 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     if (STATS) stat_add(7, t_b1 - t_b0);
     if (g + 1 < ngroups) issue_group(g + 1);
     if (ABL && (dbg & 2)) continue;
+    if (CENT && FWAV_TOPK_CSHARE && share != nullptr) {
+      // CENT: the pieces' shared limits every group (a filter threshold that rises sooner skips more level-2 work)
+#pragma unroll
+      for (int s = 0; s < QS; ++s) {
+        const uint32_t v = __hip_atomic_load(share + qpos[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (upd[s] && v != 0u) thf[s] = fmaxf(thf[s], key2f(v));
+      }
+    }
     int thi[QS];
 #pragma unroll
     for (int s = 0; s < QS; ++s) thi[s] = int_threshold(HL ? thf[s] - kStreamMargin : thf[s]);
@@ -1608,10 +1619,13 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
         }
       }
       // level 2: the marked (tile, set) pairs scored with the set's queries, kCentBatch at a time (their fragments and
-      // MFMAs in flight together; HL: the low-part fragments fetched from L2 with them), survivors appended now
+      // MFMAs in flight together).  S16: survivors appended at once.  HL: the pairs whose s16 can pass are collected
+      // first, then refined in batches of kReplayBatch with their low-part fragments fetched from L2 together (one
+      // memory round trip per batch, as the base geometry's replays) and appended.
       static_for<QS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
         uint64_t pm = pend[s];
+        uint64_t pass = 0ull;  // HL: tiles whose s16 passes the set's stream threshold
         while (pm != 0ull) {
           int t[kCentBatch];
           bool on[kCentBatch];
@@ -1621,33 +1635,55 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
             t[u] = on[u] ? __builtin_ctzll(pm) : t[0];
             if (on[u]) pm &= pm - 1;
           }
-          half8 af[kCentBatch], afl[HL ? kCentBatch : 1];
+          half8 af[kCentBatch];
           floatx16 acc[kCentBatch];
 #pragma unroll
           for (int u = 0; u < kCentBatch; ++u)
             af[u] = *reinterpret_cast<const half8*>(lda0 + (t[u] >> 3) * (512 * 8) + (t[u] & 7) * 256);
-          if constexpr (HL) {
-#pragma unroll
-            for (int u = 0; u < kCentBatch; ++u)
-              afl[u] = tile_fragment(emb16lo, (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32, h, col);
-          }
 #pragma unroll
           for (int u = 0; u < kCentBatch; ++u)
             acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], b[s], floatx16{}, 0, 0, 0);
 #pragma unroll
           for (int u = 0; u < kCentBatch; ++u) {
             if (!on[u]) break;
-            const int64_t dt = (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32;
-            floatx16 a2 = acc[u];
-            if constexpr (HL) {  // shl = s16 + d_hi·q_lo + d_lo·q_hi, refined only where some s16 can pass
-              if (__ballot(fold16((int)0x80000000, a2) > thi[s]) == 0ull) continue;
-              a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[u], bl[s], a2, 0, 0, 0);
-              a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl[u], b[s], a2, 0, 0, 0);
+            if constexpr (HL) {
+              if (__ballot(fold16((int)0x80000000, acc[u]) > thi[s]) != 0ull) pass |= 1ull << t[u];
+            } else {
+              const int64_t dt = (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32;
+              thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(acc[u], thf[s], qcnt[s], kept[s],
+                                                                                 dt, nd, gkeys, sm, wave * QS + s, K,
+                                                                                 upd[s], stats, sp, emb, qv[s],
+                                                                                 &kth[s], share);
             }
-            thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(a2, thf[s], qcnt[s], kept[s], dt,
-                                                                               nd, gkeys, sm, wave * QS + s, K,
-                                                                               upd[s], stats, sp, emb, qv[s],
-                                                                               &kth[s], share);
+          }
+        }
+        if constexpr (HL) {  // shl = s16 + d_hi·q_lo + d_lo·q_hi for the passing tiles, batched
+          while (pass != 0ull) {
+            int t[kReplayBatch];
+            bool on[kReplayBatch];
+#pragma unroll
+            for (int u = 0; u < kReplayBatch; ++u) {
+              on[u] = pass != 0ull;
+              t[u] = on[u] ? __builtin_ctzll(pass) : t[0];
+              if (on[u]) pass &= pass - 1;
+            }
+            half8 afl[kReplayBatch];
+#pragma unroll
+            for (int u = 0; u < kReplayBatch; ++u)
+              afl[u] = tile_fragment(emb16lo, (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32, h, col);
+#pragma unroll
+            for (int u = 0; u < kReplayBatch; ++u) {
+              if (!on[u]) break;
+              const half8 af = *reinterpret_cast<const half8*>(lda0 + (t[u] >> 3) * (512 * 8) + (t[u] & 7) * 256);
+              floatx16 a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, b[s], floatx16{}, 0, 0, 0);
+              a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl[s], a2, 0, 0, 0);
+              a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl[u], b[s], a2, 0, 0, 0);
+              const int64_t dt = (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32;
+              thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(a2, thf[s], qcnt[s], kept[s], dt,
+                                                                                 nd, gkeys, sm, wave * QS + s, K,
+                                                                                 upd[s], stats, sp, emb, qv[s],
+                                                                                 &kth[s], share);
+            }
           }
         }
       });
@@ -1916,12 +1952,19 @@ constexpr int g_wide = -1;
 #endif
 // first-pass geometries
 constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2;
-static int first_geometry(int64_t nd) {
+#ifndef FWAV_TOPK_CENT_HL
+#define FWAV_TOPK_CENT_HL 1  // the centroid geometry for hi/lo first passes too
+#endif
+#ifndef FWAV_TOPK_CENT_MINQ
+#define FWAV_TOPK_CENT_MINQ 0  // the centroid geometry for first passes of at least this many queries
+#endif
+static int first_geometry(int64_t nd, int64_t max_q) {
   if (g_wide >= 0) return g_wide;
   if (nd > (int64_t)FWAV_TOPK_WIDE_MIN) return kGeoWide;
-  return FWAV_TOPK_CENT > 0 ? kGeoCent : kGeoBase;
+  const bool cent = FWAV_TOPK_CENT > 0 && max_q >= (int64_t)FWAV_TOPK_CENT_MINQ &&
+                    (FWAV_TOPK_CENT_HL || first_mode(nd) == kModeS16);
+  return cent ? kGeoCent : kGeoBase;
 }
-static bool wide_geometry(int64_t nd) { return first_geometry(nd) == kGeoWide; }
 static int geometry_qb(int geo) { return geo == kGeoWide ? kWideQB : (geo == kGeoCent ? kCentQB : k16QB); }
 
 static void topk_device_slots(int geo, int& cus, int& per_cu) {
@@ -2063,7 +2106,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     (void)dbg;
 #endif
     // counter (STATS) builds of the first pass exist in the base geometry only
-    const int geo = stats_first ? kGeoBase : first_geometry(nd);
+    const int geo = stats_first ? kGeoBase : first_geometry(nd, max_q);
     const bool wide = geo == kGeoWide;
     int rt, P;
     host_plan_for(max_q, nd, geo, rt, P);
@@ -2305,7 +2348,7 @@ int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t*
 // halves), grid.
 int fwav_debug_topk_plan_info(int64_t max_q, int64_t nd, int32_t* info, int64_t* blocks) {
   FWAV_CHECK_ARG(max_q >= 0 && nd > 0 && info && blocks, FWAV_ERR_ARG, "fwav_debug_topk_plan_info: bad args");
-  const int geo = first_geometry(nd);
+  const int geo = first_geometry(nd, max_q);
   int rt, P;
   host_plan_for(max_q, nd, geo, rt, P);
   const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(geo));
@@ -2317,6 +2360,9 @@ int fwav_debug_topk_plan_info(int64_t max_q, int64_t nd, int32_t* info, int64_t*
   blocks[2] = pl.items();
   return FWAV_OK;
 }
+
+// Queries per block (one workgroup's query slots) of first-pass geometry geo (0 base, 1 wide, 2 centroid).
+int64_t fwav_debug_topk_qb(int geo) { return geo >= 0 && geo <= 2 ? geometry_qb(geo) : -1; }
 
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.

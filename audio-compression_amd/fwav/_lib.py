@@ -70,6 +70,7 @@ DEBUG_SIGNATURES = {
     "fwav_debug_topk_mode": (I32, [I32]),
     "fwav_debug_topk_geometry": (I32, [I32]),
     "fwav_debug_topk_plan_info": (I32, [I64, I64, P, P]),
+    "fwav_debug_topk_qb": (I64, [I32]),
 }
 
 
@@ -113,8 +114,11 @@ def debug_lib() -> C.CDLL:
 
 
 def lib() -> C.CDLL:
-    """The library every fwav call goes through: the product library, or the debug one inside debug_library()."""
-    return _active if _active is not None else product_lib()
+    """The library every fwav call goes through: the product library, or the debug one inside debug_library() (or
+    for the whole process under FWAV_DEBUG_LIBRARY=1: the experiment scripts in tools/ set it)."""
+    if _active is not None:
+        return _active
+    return debug_lib() if os.environ.get("FWAV_DEBUG_LIBRARY") == "1" else product_lib()
 
 
 class debug_library:

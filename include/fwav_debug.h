@@ -44,6 +44,9 @@ int fwav_debug_topk_mode(int mode);
  * sets of 4 × 32 per wave), −1 = by table size (the default).  All return the same candidates.  Re-query
  * fwav_sim_topk_workspace_size afterwards. */
 int fwav_debug_topk_geometry(int wide);
+/* Queries per block (one workgroup's query slots) of first-pass geometry geo (0 base, 1 wide, 2 centroid); −1 for
+ * another geo. */
+int64_t fwav_debug_topk_qb(int geo);
 
 #ifdef __cplusplus
 }

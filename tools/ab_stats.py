@@ -1,6 +1,8 @@
 """Slow-path counters of the fp16 search (fwav_debug_sim_topk STATS build) for several libfwav builds on the same
 inputs (pool/embeddings from the current library).  usage: [AB_CFG=cfg3] python tools/ab_stats.py lib1.so lib2.so ...
 Counters (per wave): replayed chunks, firing tiles, appends/query, compactions/query, tick shares."""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import ctypes as C
 import os
 import sys

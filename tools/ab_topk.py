@@ -1,5 +1,7 @@
 """A/B the similarity search of several libfwav builds in ONE process on the same inputs (interleaved rounds).
 usage: python tools/ab_topk.py lib1.so lib2.so ..."""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import ctypes as C
 import os
 import sys

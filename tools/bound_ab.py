@@ -4,6 +4,8 @@ tile chain, sample-chunk ordinal mod 8); the smallest of the 64 group maxima is 
 (64 distinct domains reach it).  Prints how far the bound is from the exact K-th (mean / quantiles), next to the
 exact K-th of the same sample, and times an -DFWAV_TOPK_EXTSEED build seeded with each (the prepass itself not
 included).  usage: AB_NQ=... python tools/bound_ab.py tools/ab/libfwav_ext.so F..."""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import ctypes as C
 import os
 import sys

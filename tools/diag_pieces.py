@@ -1,5 +1,7 @@
 """Compare the fp16 search with the all-f32 kernel on a golden case under several work plans (tools only).
 usage: python tools/diag_pieces.py [case] [K]"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
 import sys
 

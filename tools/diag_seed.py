@@ -1,5 +1,7 @@
 """Diagnose the seeded fp16 search against the f32 kernel on a golden case (tools only).
 usage: python tools/diag_seed.py [case] [K]"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
 import sys
 

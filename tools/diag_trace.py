@@ -1,5 +1,7 @@
 """Event trace of one query in a -DFWAV_TOPK_DEBUG=<q> build (tools/ab_build.sh): seeds, appends, compactions.
 usage: python tools/diag_trace.py tools/ab/libfwav_dbgQ.so case K Q"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import ctypes as C
 import os
 import sys

@@ -1,5 +1,7 @@
 """Counters of the exact-mode relaunch of the fp16 search (overflowed queries) on cfg3 (tools only).
 usage: python tools/ex_stats.py"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
 import sys
 

@@ -1,6 +1,8 @@
 """Counters of the fp16 search's first pass (STATS build of the kernel: replayed chunks, firing tiles, appends,
 compactions, time shares) on cfg2 for the first AB_NQ queries (tools only).
 usage: AB_NQ=41344 python tools/first_stats.py"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
 import sys
 

@@ -2,6 +2,8 @@
 for a constant τ (an -DFWAV_TOPK_EXTSEED build); prints the search time per τ and whether the candidates still equal
 the unseeded search's (they do whenever τ is below every query's K-th score − 2δ).
 usage: python tools/floor_ab.py tools/ab/libfwav_ext.so 1.70,1.80,1.85"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import ctypes as C
 import os
 import sys

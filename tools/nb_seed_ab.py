@@ -4,6 +4,8 @@ whose exact scores against query i give a valid lower bound on its K-th score (t
 seeds are computed on the device with torch from a finished search and fed to an -DFWAV_TOPK_EXTSEED build, for every
 query ("all") or for every other one ("odd": what a search that finishes the even queries first could use).
 usage: python tools/nb_seed_ab.py tools/ab/libfwav_ext.so [shifts=2]"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import ctypes as C
 import os
 import sys

@@ -8,6 +8,8 @@ The AB_NQ=41344 run of round 2 ended in a memory fault: this script sized the ke
 searched nq/2 (a table-pieces plan, which needs more: 258.4 vs 255.6 MB at cfg2), so the kernel wrote past the end
 of its workspace.  fwav_debug_sim_topk now takes the workspace size and rejects a short one; the workspace here is
 sized for every query count it searches."""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import ctypes as C
 import os
 import sys

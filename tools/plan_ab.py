@@ -1,5 +1,7 @@
 """A/B the fp16 search's work plan (fwav_debug_topk_plan) in one process on the cfg2 inputs; outputs must be
 identical to the unsplit plan.  usage: python tools/plan_ab.py "0:1,512:2,512:3" [seconds]"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
 import sys
 

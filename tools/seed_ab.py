@@ -1,6 +1,8 @@
 """Experiment (tools only): how much would a tighter initial band limit help?  Seeds every query with the K-th best
 exact score over a sample of S domains (minus 3δ, a valid s16 lower bound) computed on the host side with torch, and
 times an -DFWAV_TOPK_EXTSEED build with and without them.  usage: python tools/seed_ab.py tools/ab/libfwav_ext.so S..."""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import ctypes as C
 import os
 import sys

@@ -4,6 +4,8 @@ dbg bits (k_sim_topk_f16, STATS build): 1 = no slow path, 2 = skip MFMA + filter
 chunk, 128 = DMA every other chunk, 256 = no group barrier, 512 = fold without ballots, 1024 = MFMA without fold.
 usage: python tools/topk_ablate.py [seconds] [dbg,dbg,...] (geometry variants: tools/ab_build.sh + tools/ab_topk.py).
 Counters: replayed chunks, firing tiles, appends, compactions, per-segment tick shares, overflow fallbacks."""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os, sys, time
 sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                 os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-compression_amd")]

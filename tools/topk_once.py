@@ -1,5 +1,7 @@
 """Run the cfg2 similarity search once (after one warm-up) with a given dbg value — a target for rocprofv3 --pmc.
 usage: python tools/topk_once.py [dbg]"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
 import sys
 

@@ -1,5 +1,7 @@
 """Workgroup timeline of the similarity search (dbg 4096): how busy the GPU's workgroup slots are over time.
 usage: [PLAN=rt:P] python tools/topk_timeline.py [dbg_extra]   (prints occupancy profile + the tail's share of the kernel)"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
 import sys
 

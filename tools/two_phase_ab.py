@@ -4,6 +4,8 @@ its nearest finished neighbours' candidate rows, shifted by the distance and wid
 Q1), minus 3δ — a valid lower bound, fed through an -DFWAV_TOPK_EXTSEED build.  Times launch 1, the seed step (torch
 here; a kernel in a product) and launch 2 separately against the single launch, and checks identical candidates.
 usage: python tools/two_phase_ab.py tools/ab/libfwav_ext.so [strides=2,4,8] (AB_NQ: first nq queries)"""
+import os as _os_dbg
+_os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import ctypes as C
 import os
 import sys
