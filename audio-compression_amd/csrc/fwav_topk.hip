@@ -445,8 +445,13 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #endif
 // Centroid geometry (cent_level1): FWAV_TOPK_CENT query sets per wave (0: off), FWAV_TOPK_CW waves per
 // workgroup, FWAV_TOPK_CG chunks per barrier, FWAV_TOPK_CWPE waves per SIMD for the register allocation
+// Same-box A/B (tools/ab_topk.py, identical outputs; profiles/r04/ab_cent_*.log), search ms base → centroid:
+//   cfg2 (330,750 queries) 20.36 → 17.47 (QS 2, G 4, 2 workgroups per CU, 4 waves per SIMD), QS 4 / G 3 18.49,
+//   QS 4 / G 4 (one workgroup per CU: 2 waves per SIMD) 25.3 — the base kernel held to the same occupancy 25.6;
+//   165,375 queries 10.94 → 9.93, 82,688 5.92 → 5.69, 41,344 (one rank's eighth) 3.32 → 3.53 (fewer, longer items:
+//   the base geometry is kept below FWAV_TOPK_CENT_MINQ); cfg3 (hi/lo band, 6.6 M domains) 180 → 195 (kept base).
 #ifndef FWAV_TOPK_CENT
-#define FWAV_TOPK_CENT 0
+#define FWAV_TOPK_CENT 2
 #endif
 #ifndef FWAV_TOPK_CW
 #define FWAV_TOPK_CW 8
@@ -455,10 +460,10 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #define FWAV_TOPK_CG 4
 #endif
 #ifndef FWAV_TOPK_CWPE
-#define FWAV_TOPK_CWPE 2
+#define FWAV_TOPK_CWPE 4
 #endif
 #ifndef FWAV_TOPK_CB
-#define FWAV_TOPK_CB 2  // centroid level 2: (tile, set) pairs in flight together
+#define FWAV_TOPK_CB 4  // centroid level 2: (tile, set) pairs in flight together (2: +0.5 % at cfg2)
 #endif
 #ifndef FWAV_TOPK_CSHARE
 #define FWAV_TOPK_CSHARE 1  // centroid geometry: read the pieces' shared limits every group (else at window ends)
@@ -1953,10 +1958,10 @@ constexpr int g_wide = -1;
 // first-pass geometries
 constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2;
 #ifndef FWAV_TOPK_CENT_HL
-#define FWAV_TOPK_CENT_HL 1  // the centroid geometry for hi/lo first passes too
+#define FWAV_TOPK_CENT_HL 0  // the centroid geometry for hi/lo first passes too (cfg3: 195 vs 180 ms base)
 #endif
 #ifndef FWAV_TOPK_CENT_MINQ
-#define FWAV_TOPK_CENT_MINQ 0  // the centroid geometry for first passes of at least this many queries
+#define FWAV_TOPK_CENT_MINQ 60000  // the centroid geometry for first passes of at least this many queries
 #endif
 static int first_geometry(int64_t nd, int64_t max_q) {
   if (g_wide >= 0) return g_wide;

@@ -81,14 +81,38 @@ def defer(finish, device: torch.device):
     return _driver().submit(job)
 
 
+def _cpu_share() -> int:
+    """CPUs this process may use: the cgroup's CPU quota (cpu.max) when it sets one, else the affinity mask (the GPU
+    boxes report 256 CPUs to os.cpu_count() but give a job a 16-CPU quota)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def tie_threads() -> int:
+    """Host threads ranking exact score rows in this process: FWAV_TIE_THREADS, else the CPU share divided among the
+    node's ranks (LOCAL_WORLD_SIZE), at most 8.  Measured on a GPU box with cfg4 rows (86.4 M scores,
+    tools/host_rank_contention.py, profiles/r04/host_rank_contention.log): one process 8 threads 47 ms per row; eight
+    processes at once 8 threads each 354 ms, 2 threads each 166 ms, 1 thread each 283 ms."""
+    env = os.environ.get("FWAV_TIE_THREADS")
+    if env:
+        return max(1, int(env))
+    ranks = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    return max(1, min(8, _cpu_share() // ranks))
+
+
 def _pool():
-    """Host threads for numpy's ranking of the exact score rows (argpartition runs outside the GIL; measured on the
-    box's 16-CPU share: 8 threads 5.7x one at cfg2 row widths, `profiles/r03/host_tie_cost.log`)."""
+    """Host threads for numpy's ranking of the exact score rows (argpartition runs outside the GIL): tie_threads()."""
     global _POOL
     if _POOL is None:
         from concurrent.futures import ThreadPoolExecutor
-        n = int(os.environ.get("FWAV_TIE_THREADS", str(min(8, os.cpu_count() or 1))))
-        _POOL = ThreadPoolExecutor(max(1, n), thread_name_prefix="fwav-ties")
+        _POOL = ThreadPoolExecutor(tie_threads(), thread_name_prefix="fwav-ties")
     return _POOL
 
 
