@@ -505,7 +505,10 @@ constexpr int kGrow = FWAV_TOPK_GROW;  // ... and growth since the last compacti
 static_assert(k16Cap >= 128 && (k16Cap & (k16Cap - 1)) == 0, "the final bitonic sort needs a power-of-two buffer");
 // (A/B at cfg2: 512 entries 24.4 ms vs 21.2 ms for 256 — fewer compactions do not pay for the longer final sort)
 constexpr int k16QB = 32 * k16Waves * k16Sets;  // queries per block (one workgroup's query set)
-constexpr int kMaxPieces = 8;        // a split block's table pieces (merge: P·K ≤ 512 keys per query)
+#ifndef FWAV_TOPK_MAXP
+#define FWAV_TOPK_MAXP 8
+#endif
+constexpr int kMaxPieces = FWAV_TOPK_MAXP;  // a split block's table pieces (merge: P·(C − 64) keys per query at most)
 
 // Work plan of the fp16 search.  The n_blocks query blocks are items of one launch, dispatched in order: the first
 // F = nb − R blocks stream the whole table, then each of the last R = min(nb, rt) blocks is split into P pieces of
@@ -1950,13 +1953,20 @@ constexpr int kWideW = 16, kWideG = 8;
 constexpr int kWideQB = 32 * kWideW;
 constexpr int kCentQS = FWAV_TOPK_CENT > 0 ? FWAV_TOPK_CENT : 4, kCentW = FWAV_TOPK_CW, kCentG = FWAV_TOPK_CG;
 constexpr int kCentQB = 32 * kCentW * kCentQS;
+constexpr int kCentWideQB = 32 * kWideW * kCentQS;  // the centroid filter in the wide geometry (16 waves, 8 chunks)
 #ifdef FWAV_DEBUG_API
 static int g_wide = -1;  // fwav_debug_topk_geometry (debug library only): force base / wide / centroid
 #else
 constexpr int g_wide = -1;
 #endif
 // first-pass geometries
-constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2;
+constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2, kGeoCentWide = 3;
+#ifndef FWAV_TOPK_CPDBL
+#define FWAV_TOPK_CPDBL 4  // centroid geometry, blocks on at most half the slots: pieces doubled below this count
+#endif
+#ifndef FWAV_TOPK_CENTWIDE
+#define FWAV_TOPK_CENTWIDE 0  // tables past the Infinity Cache: the centroid filter in the wide geometry
+#endif
 #ifndef FWAV_TOPK_CENT_HL
 #define FWAV_TOPK_CENT_HL 0  // the centroid geometry for hi/lo first passes too (cfg3: 195 vs 180 ms base)
 #endif
@@ -1965,15 +1975,17 @@ constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2;
 #endif
 static int first_geometry(int64_t nd, int64_t max_q) {
   if (g_wide >= 0) return g_wide;
-  if (nd > (int64_t)FWAV_TOPK_WIDE_MIN) return kGeoWide;
+  if (nd > (int64_t)FWAV_TOPK_WIDE_MIN) return FWAV_TOPK_CENTWIDE ? kGeoCentWide : kGeoWide;
   const bool cent = FWAV_TOPK_CENT > 0 && max_q >= (int64_t)FWAV_TOPK_CENT_MINQ &&
                     (FWAV_TOPK_CENT_HL || first_mode(nd) == kModeS16);
   return cent ? kGeoCent : kGeoBase;
 }
-static int geometry_qb(int geo) { return geo == kGeoWide ? kWideQB : (geo == kGeoCent ? kCentQB : k16QB); }
+static int geometry_qb(int geo) {
+  return geo == kGeoWide ? kWideQB : (geo == kGeoCent ? kCentQB : (geo == kGeoCentWide ? kCentWideQB : k16QB));
+}
 
 static void topk_device_slots(int geo, int& cus, int& per_cu) {
-  static int cs[3][kMaxDev] = {{0}}, ws[3][kMaxDev] = {{0}};
+  static int cs[4][kMaxDev] = {{0}}, ws[4][kMaxDev] = {{0}};
   const int dev = current_device();
   int& c = cs[geo][dev];
   int& w = ws[geo][dev];
@@ -1985,12 +1997,15 @@ static void topk_device_slots(int geo, int& cus, int& per_cu) {
         : geo == kGeoCent
             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                   &w, k_sim_topk_f16<k16Cap, false, kModeS16, kCentW, kCentG, kCentQS, true>, 64 * kCentW, 0)
+        : geo == kGeoCentWide
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                  &w, k_sim_topk_f16<k16Cap, false, kModeHL, kWideW, kWideG, kCentQS, true>, 64 * kWideW, 0)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeS16>, 64 * k16Waves,
                                                            0);
     if (!(hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && occ == hipSuccess &&
           c > 0 && w > 0)) {
       c = 256;  // MI355X: 256 CUs × 2 base (1 wide) workgroups
-      w = geo == kGeoBase ? 2 : 1;
+      w = (geo == kGeoBase || geo == kGeoCent) ? 2 : 1;
     }
   }
   cus = c;
@@ -2004,7 +2019,6 @@ static void topk_device_slots(int geo, int& cus, int& per_cu) {
 // since every piece restarts the rising limit: 268 blocks in 2 pieces 24.2 ms, 512 in 2 25.3 ms).  Few blocks
 // (at most half the slots) are each split into up to 8 pieces so that the table passes use the idle CUs.
 static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
-  const bool wide = geo == kGeoWide;
   if (g_plan_rt >= 0) {  // diagnostic override
     rt = g_plan_rt;
     P = g_plan_p;
@@ -2022,7 +2036,7 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
       // 65,536: 5.29 → 4.83 with 4 instead of 2; 20,672: 2.25 → 2.08 with 6, block-major before)
       rt = (int)nb;
       int64_t p = slots / nb;
-      if (FWAV_TOPK_PMAJOR && p < 4) p *= 2;
+      if (FWAV_TOPK_PMAJOR && p < (geo == kGeoCent ? FWAV_TOPK_CPDBL : 4)) p *= 2;
       P = (int)(p < kMaxPieces ? p : kMaxPieces);
     } else if (FWAV_TOPK_PMAJOR && 2 * nb <= 3 * slots) {
       // up to 1.5 rounds of blocks: every block in max(3, ⌊2·slots / nb⌋) pieces, piece-major — later rounds start
@@ -2061,7 +2075,7 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
 static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
   const int64_t q = max_q > 0 ? max_q : 1;
   size_t items_q = (size_t)make_plan(q, 0, 1, k16QB).items() * k16QB;
-  for (int geo = 0; geo < 3; ++geo) {
+  for (int geo = 0; geo < 4; ++geo) {
     int rt, P;
     host_plan_for(q, nd, geo, rt, P);
     const int qb = geometry_qb(geo);
@@ -2129,6 +2143,10 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
   k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG, 1><<<pl.items(), 64 * kWideW, 0, st>>>(                    \
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
       sp, ties)
+#define FWAV_FIRST_CENTW(MODE_)                                                                                  \
+  k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG, kCentQS, true><<<pl.items(), 64 * kWideW, 0, st>>>(        \
+      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
+      sp, ties)
 #define FWAV_FIRST_CENT(MODE_)                                                                                   \
   k_sim_topk_f16<k16Cap, false, MODE_, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(        \
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
@@ -2148,12 +2166,15 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       if (mode1 == kModeHL) FWAV_FIRST_WIDE(kModeHL); else FWAV_FIRST_WIDE(kModeS16);
     } else if (geo == kGeoCent) {
       if (mode1 == kModeHL) FWAV_FIRST_CENT(kModeHL); else FWAV_FIRST_CENT(kModeS16);
+    } else if (geo == kGeoCentWide) {
+      if (mode1 == kModeHL) FWAV_FIRST_CENTW(kModeHL); else FWAV_FIRST_CENTW(kModeS16);
     } else {
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, nullptr); else FWAV_FIRST(kModeS16, false, 0, nullptr);
     }
 #undef FWAV_FIRST
 #undef FWAV_FIRST_WIDE
 #undef FWAV_FIRST_CENT
+#undef FWAV_FIRST_CENTW
     if (pl.R > 0) {
 #define FWAV_MERGE(QB_, HL_)                                                                                    \
   k_merge_pieces<k16Cap, QB_, HL_><<<cdiv(pl.R * QB_, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, \
@@ -2162,6 +2183,8 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
         if (mode1 == kModeHL) FWAV_MERGE(kWideQB, true); else FWAV_MERGE(kWideQB, false);
       } else if (geo == kGeoCent) {
         if (mode1 == kModeHL) FWAV_MERGE(kCentQB, true); else FWAV_MERGE(kCentQB, false);
+      } else if (geo == kGeoCentWide) {
+        if (mode1 == kModeHL) FWAV_MERGE(kCentWideQB, true); else FWAV_MERGE(kCentWideQB, false);
       } else {
         if (mode1 == kModeHL) FWAV_MERGE(k16QB, true); else FWAV_MERGE(k16QB, false);
       }
@@ -2315,7 +2338,7 @@ int fwav_debug_topk_mode(int mode) {
 // Diagnostic override of the first pass's geometry: 0 = base (8 waves, 256 queries per workgroup), 1 = wide (16
 // waves, 512 queries, one workgroup per CU), −1 = by table size (default).  Both return the same candidates.
 int fwav_debug_topk_geometry(int wide) {
-  FWAV_CHECK_ARG(wide >= -1 && wide <= 2, FWAV_ERR_ARG, "fwav_debug_topk_geometry: outside [-1, 2]");
+  FWAV_CHECK_ARG(wide >= -1 && wide <= 3, FWAV_ERR_ARG, "fwav_debug_topk_geometry: outside [-1, 3]");
   g_wide = wide;
   return FWAV_OK;
 }
@@ -2325,12 +2348,12 @@ int fwav_debug_topk_geometry(int wide) {
 // A query of a whole-table block or a query half must be counted once, one of a block split into P table pieces P
 // times.  *items = the launch's grid.
 int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t* count, int64_t* items) {
-  FWAV_CHECK_ARG(n >= 0 && count && items && wide >= 0 && wide <= 2 &&
+  FWAV_CHECK_ARG(n >= 0 && count && items && wide >= 0 && wide <= 3 &&
                      (pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces)), FWAV_ERR_ARG,
                  "fwav_debug_topk_plan_cover: bad args");
-  const int geo = wide;  // 0 base, 1 wide, 2 centroid
-  const int W = geo == kGeoWide ? kWideW : (geo == kGeoCent ? kCentW : k16Waves);
-  const int sets = geo == kGeoCent ? kCentQS : k16Sets, qb = 32 * W * sets;
+  const int geo = wide;  // 0 base, 1 wide, 2 centroid, 3 centroid wide
+  const int W = (geo == kGeoWide || geo == kGeoCentWide) ? kWideW : (geo == kGeoCent ? kCentW : k16Waves);
+  const int sets = (geo == kGeoCent || geo == kGeoCentWide) ? kCentQS : k16Sets, qb = 32 * W * sets;
   const TopkPlan pl = make_plan(n, rt, pieces, qb);
   *items = pl.items();
   for (int64_t it = 0; it < pl.items(); ++it) {
@@ -2367,7 +2390,7 @@ int fwav_debug_topk_plan_info(int64_t max_q, int64_t nd, int32_t* info, int64_t*
 }
 
 // Queries per block (one workgroup's query slots) of first-pass geometry geo (0 base, 1 wide, 2 centroid).
-int64_t fwav_debug_topk_qb(int geo) { return geo >= 0 && geo <= 2 ? geometry_qb(geo) : -1; }
+int64_t fwav_debug_topk_qb(int geo) { return geo >= 0 && geo <= 3 ? geometry_qb(geo) : -1; }
 
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.

@@ -27,13 +27,13 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, 
  * same candidates.  Re-query fwav_sim_topk_workspace_size afterwards. */
 int fwav_debug_topk_plan(int rt, int pieces);
 /* The first pass fwav_sim_topk would launch for max_q queries over n_domains domains on the current device (host
- * only): info[0] = geometry (0 = base, 1 = wide, 2 = centroid), info[1] = first-pass mode (0 = fp16 band, 1 = hi/lo band), info[2] = table
+ * only): info[0] = geometry (0 = base, 1 = wide, 2 = centroid, 3 = centroid wide), info[1] = first-pass mode (0 = fp16 band, 1 = hi/lo band), info[2] = table
  * pieces per split block (−1: query halves); blocks[0] = whole-table blocks, blocks[1] = split blocks,
  * blocks[2] = grid. */
 int fwav_debug_topk_plan_info(int64_t max_q, int64_t n_domains, int32_t* info, int64_t* blocks);
 /* Host-side check of a work plan (no device): count[position] += 1 for every query slot of every item of the plan of
  * n queries (whole blocks and query halves cover a query once, a block in P table pieces P times) in first-pass
- * geometry `wide` (0 = base, 1 = wide, 2 = centroid); *items = grid. */
+ * geometry `wide` (0 = base, 1 = wide, 2 = centroid, 3 = centroid wide); *items = grid. */
 int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t* count, int64_t* items);
 /* Diagnostic override of the fp16 search's first-pass mode: 0 = fp16 band (overflowing queries relaunched with the
  * hi/lo band, then exact keys), 1 = hi/lo band (then exact keys), −1 = by table size (the default: hi/lo above 4 Mi
@@ -41,11 +41,12 @@ int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t*
 int fwav_debug_topk_mode(int mode);
 /* Diagnostic override of the fp16 search's first-pass geometry: 0 = 8 waves × 32 queries per workgroup, 1 = 16 waves
  * × 32 queries, one workgroup per CU (the table streamed once per 512 queries), 2 = the centroid pre-filter (query
- * sets of 4 × 32 per wave), −1 = by table size (the default).  All return the same candidates.  Re-query
+ * sets of 2 × 32 per wave), 3 = the centroid pre-filter in the wide geometry, −1 = by table size and query count (the
+ * default).  All return the same candidates.  Re-query
  * fwav_sim_topk_workspace_size afterwards. */
 int fwav_debug_topk_geometry(int wide);
-/* Queries per block (one workgroup's query slots) of first-pass geometry geo (0 base, 1 wide, 2 centroid); −1 for
- * another geo. */
+/* Queries per block (one workgroup's query slots) of first-pass geometry geo (0 base, 1 wide, 2 centroid,
+ * 3 centroid wide); −1 for another geo. */
 int64_t fwav_debug_topk_qb(int geo);
 
 #ifdef __cplusplus

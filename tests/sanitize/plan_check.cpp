@@ -29,13 +29,13 @@ int main() {
   for (int64_t nd : nds) {
     for (int64_t q : qs) {
       if (q > 3 * nd) continue;
-      for (int geo = -1; geo <= 2; ++geo) {
+      for (int geo = -1; geo <= 3; ++geo) {
         CHECK(fwav_debug_topk_geometry(geo) == FWAV_OK, "geometry %d", geo);
         int32_t info[3] = {-9, -9, -9};
         int64_t blocks[3] = {-9, -9, -9};
         CHECK(fwav_debug_topk_plan_info(q, nd, info, blocks) == FWAV_OK, "plan_info");
         const int g = info[0], P = info[2] < 0 ? -1 : info[2];
-        CHECK(g >= 0 && g <= 2 && (geo < 0 || g == geo), "geometry %d for %d", g, geo);
+        CHECK(g >= 0 && g <= 3 && (geo < 0 || g == geo), "geometry %d for %d", g, geo);
         const int64_t F = blocks[0], R = blocks[1], items = blocks[2];
         CHECK(F >= 0 && R >= 0 && items >= F + R, "blocks F=%lld R=%lld items=%lld", (long long)F, (long long)R,
               (long long)items);
@@ -54,7 +54,8 @@ int main() {
               (long long)bad);
         // the workspace holds the plan's key buffers (256 keys of 8 B per query slot) in every geometry
         const size_t ws = fwav_sim_topk_workspace_size(q, nd, 64);
-        const int qb = g == 1 ? 512 : (g == 2 ? 1024 : 256);
+        const int qb = (int)fwav_debug_topk_qb(g);
+        CHECK(qb >= 256 && qb % 256 == 0, "qb %d", qb);
         CHECK(ws >= (size_t)items * qb * 256 * 8, "workspace %zu < %lld items x %d", ws, (long long)items, qb);
         ++plans;
       }
@@ -64,7 +65,7 @@ int main() {
   // every work-plan override returns a covering plan
   for (int pieces : {-1, 1, 2, 3, 5, 8}) {
     for (int rt : {0, 1, 7, 1 << 20}) {
-      for (int geo = 0; geo <= 2; ++geo) {
+      for (int geo = 0; geo <= 3; ++geo) {
         const int64_t n = 41344;
         std::vector<int32_t> count((size_t)n, 0);
         int64_t it = 0;
@@ -76,7 +77,7 @@ int main() {
   // argument checks: rejected before any HIP call, with a message
   CHECK(fwav_debug_topk_plan_cover(-1, 0, 1, 0, nullptr, nullptr) == FWAV_ERR_ARG, "cover args");
   CHECK(fwav_debug_topk_plan_cover(10, 0, 9, 0, nullptr, nullptr) == FWAV_ERR_ARG, "cover pieces");
-  CHECK(fwav_debug_topk_geometry(3) == FWAV_ERR_ARG, "geometry range");
+  CHECK(fwav_debug_topk_geometry(4) == FWAV_ERR_ARG, "geometry range");
   CHECK(fwav_debug_topk_mode(2) == FWAV_ERR_ARG, "mode range");
   CHECK(fwav_debug_topk_plan(0, 9) == FWAV_ERR_ARG, "plan pieces");
   CHECK(fwav_sim_topk(nullptr, nullptr, 10, nullptr, nullptr, 10, 0, 64, 1, nullptr, nullptr, nullptr, 0, nullptr) ==

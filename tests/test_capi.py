@@ -172,7 +172,7 @@ def test_workspace_sizes(lib):
     assert size_call("fwav_sim_topk_workspace_size", 10, 1000, 1000) == 10 * 1000 * 4
 
 
-@pytest.mark.parametrize("wide", [0, 1, 2])
+@pytest.mark.parametrize("wide", [0, 1, 2, 3])
 @pytest.mark.parametrize("n,rt,pieces", [(330750, 0, 1), (330750, 24, 4), (41344, 1 << 20, 3), (165375, 134, 4),
                                          (1000, 1 << 20, 8), (70000, 7, -1), (33, 3, 2), (256 * 5, 2, 5)])
 def test_work_plan_covers_every_query(lib, n, rt, pieces, wide):
@@ -183,7 +183,7 @@ def test_work_plan_covers_every_query(lib, n, rt, pieces, wide):
     with lib.debug_library():
         lib.call("fwav_debug_topk_plan_cover", n, rt, pieces, wide, count.ctypes.data, ctypes.addressof(items))
     qb = lib.debug_lib().fwav_debug_topk_qb(wide)  # queries per block of the geometry
-    assert qb == 32 * (16 if wide == 1 else 8) * (1 if wide != 2 else qb // 256)
+    assert qb == 32 * (16 if wide in (1, 3) else 8) * (1 if wide < 2 else qb // (512 if wide == 3 else 256))
     nb = -(-n // qb)
     P = 1 if pieces == 1 else (2 if pieces == -1 else pieces)
     R = 0 if P == 1 else min(nb, rt)

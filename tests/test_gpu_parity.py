@@ -150,8 +150,9 @@ def _cands(sig, tile, K, search, thr=1e-4, tie_order="numpy_sets"):
     return r.cand.cpu().numpy().reshape(-1, K), r
 
 
-@pytest.fixture(params=[(-1, -1), (0, 0), (1, 0), (0, 1), (1, 1), (0, 2), (1, 2)],
-                ids=["auto", "s16-base", "hl-base", "s16-wide", "hl-wide", "s16-cent", "hl-cent"])
+@pytest.fixture(params=[(-1, -1), (0, 0), (1, 0), (0, 1), (1, 1), (0, 2), (1, 2), (0, 3), (1, 3)],
+                ids=["auto", "s16-base", "hl-base", "s16-wide", "hl-wide", "s16-cent", "hl-cent", "s16-centw",
+                     "hl-centw"])
 def first_mode(request):
     """Run a test under each first-pass mode (fwav_debug_topk_mode) and workgroup geometry (fwav_debug_topk_geometry)
     of the fp16 search, then restore the defaults."""
@@ -247,7 +248,7 @@ def test_large_k_vs_oracle(K):
         assert bit_equal(t.cpu().numpy(), np.asarray(b))
 
 
-@pytest.mark.parametrize("wide", [0, 1, 2], ids=["base", "wide", "cent"])
+@pytest.mark.parametrize("wide", [0, 1, 2, 3], ids=["base", "wide", "cent", "centw"])
 @pytest.mark.parametrize("plan", [(0, 1), (1 << 20, 2), (1 << 20, 5), (1 << 20, 8), (10, 3), (1 << 20, -1), (7, -1)])
 def test_f16_split_plans_equal_f32(plan, wide):
     """Work plans that split query blocks into table pieces (merged by k_merge_pieces) or into query halves return
