@@ -1965,7 +1965,10 @@ constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2, kGeoCentWide = 3;
 #define FWAV_TOPK_CPDBL 4  // centroid geometry, blocks on at most half the slots: pieces doubled below this count
 #endif
 #ifndef FWAV_TOPK_CENTWIDE
-#define FWAV_TOPK_CENTWIDE 0  // tables past the Infinity Cache: the centroid filter in the wide geometry
+// tables past the Infinity Cache: the centroid filter in the wide geometry (16 waves × 2 sets of 32, 8-chunk groups,
+// one workgroup per CU).  A cfg4 shard (337,500 queries × 86.4 M domains, hi/lo band, identical outputs): wide
+// 920 ms → centroid wide 632 ms (profiles/r04/ab_centwide_cfg4_q337500.log)
+#define FWAV_TOPK_CENTWIDE 1
 #endif
 #ifndef FWAV_TOPK_CENT_HL
 #define FWAV_TOPK_CENT_HL 0  // the centroid geometry for hi/lo first passes too (cfg3: 195 vs 180 ms base)
@@ -1975,7 +1978,8 @@ constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2, kGeoCentWide = 3;
 #endif
 static int first_geometry(int64_t nd, int64_t max_q) {
   if (g_wide >= 0) return g_wide;
-  if (nd > (int64_t)FWAV_TOPK_WIDE_MIN) return FWAV_TOPK_CENTWIDE ? kGeoCentWide : kGeoWide;
+  if (nd > (int64_t)FWAV_TOPK_WIDE_MIN)
+    return FWAV_TOPK_CENTWIDE && max_q >= (int64_t)FWAV_TOPK_CENT_MINQ ? kGeoCentWide : kGeoWide;
   const bool cent = FWAV_TOPK_CENT > 0 && max_q >= (int64_t)FWAV_TOPK_CENT_MINQ &&
                     (FWAV_TOPK_CENT_HL || first_mode(nd) == kModeS16);
   return cent ? kGeoCent : kGeoBase;

@@ -190,6 +190,7 @@ def rank_rows(launches, n: int, n_domains: int, k: int, copy_stream=None) -> lis
                           flush=True)
                 for i, sl, h in hs:
                     futs[i] = _SLOT_BUSY[sl] = ex.submit(numpy_topk_row, h.numpy(), k)
+            src = None  # (a view of S: would keep the launch's rows allocated while the next launch allocates)
             del S
         _SLOT_NEXT = (base + n) % nslots
     return futs

@@ -243,10 +243,10 @@ def test_cfg2_whole_search_equals_f32():
 
 def test_cfg4_shard_wide_geometry_default():
     """A cfg4 shard of 337,500 consecutive queries (one rank's share of 64) against the whole 86.4 M-domain table —
-    where the wide geometry (16 waves × 32 queries, one workgroup per CU) is the default first pass.  The plan is
-    asserted to be the wide one with whole-table blocks; every row equals the base-geometry search (8 waves, a
-    different plan and processing order), 1,024 rows equal the all-f32 kernel, and sampled rows hold the exact top
-    K (fractal.py:535-541)."""
+    where the centroid filter in the wide geometry (16 waves × 2 sets of 32 queries, one workgroup per CU) is the
+    default first pass.  The plan is asserted to be that one with whole-table blocks; every row equals the
+    base-geometry search (8 waves, no centroids, a different plan and processing order), 1,024 rows equal the all-f32
+    kernel, and sampled rows hold the exact top K (fractal.py:535-541)."""
     sig, _, _ = synth.make_config_signal("cfg4", seed=0)
     q = 337_500
     x = torch.from_numpy(sig).to(dev())
@@ -259,7 +259,7 @@ def test_cfg4_shard_wide_geometry_default():
         call("fwav_debug_topk_plan_info", q, nd, info.ctypes.data, blocks.ctypes.data)
     print(f"cfg4 shard plan: wide {info[0]} mode {info[1]} pieces {info[2]} whole blocks {blocks[0]} split "
           f"{blocks[1]} grid {blocks[2]}")
-    assert info[0] == 1 and blocks[0] > 0 and blocks[0] * 512 >= q // 2
+    assert info[0] == 3 and blocks[0] > 0 and blocks[0] * 1024 >= q // 2  # the centroid filter, wide geometry
     wide = res.cand.view(-1, K).cpu().numpy()
     assert (wide >= 0).all() and (wide < nd).all()
     with debug_library():
