@@ -259,7 +259,8 @@ def test_cfg4_shard_wide_geometry_default():
         call("fwav_debug_topk_plan_info", q, nd, info.ctypes.data, blocks.ctypes.data)
     print(f"cfg4 shard plan: wide {info[0]} mode {info[1]} pieces {info[2]} whole blocks {blocks[0]} split "
           f"{blocks[1]} grid {blocks[2]}")
-    assert info[0] == 3 and blocks[0] > 0 and blocks[0] * 1024 >= q // 2  # the centroid filter, wide geometry
+    # the centroid filter in the wide geometry: 330 blocks of 1,024 queries on 256 slots, every block in table pieces
+    assert info[0] == 3 and blocks[0] + blocks[1] == -(-q // 1024) and blocks[2] >= blocks[0] + blocks[1]
     wide = res.cand.view(-1, K).cpu().numpy()
     assert (wide >= 0).all() and (wide < nd).all()
     with debug_library():

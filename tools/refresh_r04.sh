@@ -18,3 +18,4 @@ step bench_r04 500 python -u bench.py --steps 20 --warmup 5
 step prof_r04 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r04 -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
 step pmc_fetch_r04 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch_r04 -- python3 bench.py --no-cpu-baseline --no-extras --steps 2 --warmup 1
 step pmc_write_r04 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write_r04 -- python3 bench.py --no-cpu-baseline --no-extras --steps 2 --warmup 1
+step shard_step_r04 600 python -u tools/shard_step.py --steps 20
