@@ -1970,6 +1970,9 @@ constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2, kGeoCentWide = 3;
 // 920 ms → centroid wide 632 ms (profiles/r04/ab_centwide_cfg4_q337500.log)
 #define FWAV_TOPK_CENTWIDE 1
 #endif
+#ifndef FWAV_TOPK_CPMIN
+#define FWAV_TOPK_CPMIN 6  // centroid geometry, up to 1.5 rounds of blocks: at least this many table pieces each
+#endif
 #ifndef FWAV_TOPK_CENT_HL
 #define FWAV_TOPK_CENT_HL 0  // the centroid geometry for hi/lo first passes too (cfg3: 195 vs 180 ms base)
 #endif
@@ -2047,9 +2050,14 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
       // from the earlier pieces' limits (82,688 queries: 6.43 → 5.92 ms with 3 pieces; 165,375: 11.27 → 10.81 with
       // 3, 10.72 with 4; the tail split below stays for more blocks: all of cfg2 in 2 / 3 / 4 piece-major pieces
       // 20.8 / 20.5 / 20.7 vs 20.2–20.4 ms)
+      // The centroid geometry takes at least 6 (its first pass is cheap, so the table pieces' restarted limits weigh
+      // less than the balance of ≈ 4–8 rounds of short items: cfg2 646 blocks in 3 / 4 / 5 / 6 / 8 pieces 17.37 /
+      // 16.94 / 17.02 / 16.89 / 17.40 ms, 165,375 queries in 3 / 4 / 6 10.04 / 9.92 / 9.68;
+      // profiles/r04/plan_sweep_cent_cfg2.log)
       rt = (int)nb;
       int64_t p = 2 * slots / nb;
-      if (p < 3) p = 3;
+      const int64_t pmin = (geo == kGeoCent) ? FWAV_TOPK_CPMIN : 3;
+      if (p < pmin) p = pmin;
       P = (int)(p < kMaxPieces ? p : kMaxPieces);
     } else {
       const int64_t last = nb % slots == 0 ? slots : nb % slots;  // blocks in the last round

@@ -61,6 +61,8 @@ for _, L in libs:
     L.fwav_sim_topk_workspace_size.argtypes = [C.c_int64, C.c_int64, C.c_int]
     if os.environ.get("AB_PLAN"):
         L.fwav_debug_topk_plan(*[int(x) for x in os.environ["AB_PLAN"].split(",")])
+    if os.environ.get("AB_GEO"):  # first-pass geometry override (0 base, 1 wide, 2 centroid, 3 centroid wide)
+        L.fwav_debug_topk_geometry(int(os.environ["AB_GEO"]))
     wsn = max(wsn, L.fwav_sim_topk_workspace_size(nq, nd, 64))
 wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
 outs = {}
