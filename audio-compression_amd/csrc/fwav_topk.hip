@@ -417,7 +417,9 @@ __device__ uint32_t g_fwav_dbg_n;
 //   [9] ticks streaming (MFMA + filter, between barrier and window end)   (s_memrealtime ticks, 100 MHz)
 // `stats` inside the kernel is the wave's own LDS counter row (lane 0 adds; flushed once per wave at the end),
 // so the instrumentation adds no global atomics to the measured loop.
-constexpr int kStats = 12;
+// [12] ticks waiting for the group's own chunk DMA (vmcnt at the group top; [7] is then the barrier alone),
+//   [13] centroid level-1 ticks, [14] centroid level-2 (tile, set) pairs
+constexpr int kStats = 16;
 __device__ __forceinline__ void stat_add_p(unsigned long long* stats, int i, unsigned long long v) {
   if (stats != nullptr && (threadIdx.x & 63) == 0) stats[i] += v;
 }
@@ -621,7 +623,7 @@ __device__ __forceinline__ bool may_pass(int imx, float thf) {
 
 // NG = query groups of 32 per workgroup (W waves × QS sets).  Kept small: two workgroups (2 × 64 KB of chunk
 // slots + this) must fit one CU's 160 KB of LDS.
-template <int NG, bool STATS, bool FIFO = true>
+template <int NG, bool STATS, bool FIFO = true, int NW = NG>
 struct Topk16SmemT {
   int cnt[32 * NG];   // final pass: entries at the front of the query's buffer (its h = 0 lane's appends)
   int cnt1[32 * NG];  // ... and at the back (its h = 1 lane's)
@@ -632,7 +634,7 @@ struct Topk16SmemT {
   int64_t qrow[32 * NG];
   int32_t qpos[32 * NG];  // position of the slot's query in the active list (index of its shared band limit)
   uint32_t fired[FIFO ? NG : 1][kFifo];            // deferred work: ring of fired chunk entries (not in CENT)
-  unsigned long long wstat[STATS ? NG : 1][kStats];  // STATS builds only (one row per wave)
+  unsigned long long wstat[STATS ? NW : 1][kStats];  // STATS builds only (one row per wave)
 };
 
 // Streaming compaction on shl keys (no f32 rescoring, no table loads, no sort): S = the K-th largest shl in the
@@ -1423,11 +1425,11 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
   struct Lds {
     u32x4 slots[2 * G][512];
-    Topk16SmemT<NG, STATS, !CENT> sm;
+    Topk16SmemT<NG, STATS, !CENT, W> sm;
   };
   __shared__ __attribute__((aligned(16))) Lds lds_all;
   u32x4(*slots)[512] = lds_all.slots;
-  Topk16SmemT<NG, STATS, !CENT>& sm = lds_all.sm;
+  Topk16SmemT<NG, STATS, !CENT, W>& sm = lds_all.sm;
 
   const int n_active = *n_active_p;
   constexpr int QB = 32 * NG;  // queries per block
@@ -1589,6 +1591,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     // iteration g−1, whose ds_reads were all consumed before its waves reached this barrier.
     if (!(ABL && (dbg & 256))) {  // ablation 256: no group barrier (LDS races; timing only)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (STATS) stat_add(12, __builtin_amdgcn_s_memrealtime() - t_b0);
       if (!(ABL && (dbg & 16384))) __builtin_amdgcn_s_barrier();  // 16384: own DMA wait, no barrier
       asm volatile("" ::: "memory");
     }
@@ -1614,6 +1617,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       for (int s = 0; s < QS; ++s) tv[s] = HL ? thf[s] - kStreamMargin : thf[s];
       const int thc = centroid_threshold<QS>(tv, cslack);
       uint64_t pend[QS];
+      const unsigned long long t_l1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
       if (c_end - cg == G) {
         cent_level1<G, QS>(lda0, bc, thc, pend);
       } else {
@@ -1625,6 +1629,13 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
 #pragma unroll
           for (int s = 0; s < QS; ++s) pend[s] |= pc[s] << (8 * (c - cg));
         }
+      }
+      if (STATS) {
+        stat_add(13, __builtin_amdgcn_s_memrealtime() - t_l1);
+        unsigned long long np = 0;
+#pragma unroll
+        for (int s = 0; s < QS; ++s) np += __popcll(pend[s]);
+        stat_add(14, np);
       }
       // level 2: the marked (tile, set) pairs scored with the set's queries, kCentBatch at a time (their fragments and
       // MFMAs in flight together).  S16: survivors appended at once.  HL: the pairs whose s16 can pass are collected
@@ -1658,7 +1669,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
               if (__ballot(fold16((int)0x80000000, acc[u]) > thi[s]) != 0ull) pass |= 1ull << t[u];
             } else {
               const int64_t dt = (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32;
-              thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(acc[u], thf[s], qcnt[s], kept[s],
+              thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT, W>, MODE>(acc[u], thf[s], qcnt[s], kept[s],
                                                                                  dt, nd, gkeys, sm, wave * QS + s, K,
                                                                                  upd[s], stats, sp, emb, qv[s],
                                                                                  &kth[s], share);
@@ -1687,7 +1698,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
               a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl[s], a2, 0, 0, 0);
               a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl[u], b[s], a2, 0, 0, 0);
               const int64_t dt = (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32;
-              thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(a2, thf[s], qcnt[s], kept[s], dt,
+              thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT, W>, MODE>(a2, thf[s], qcnt[s], kept[s], dt,
                                                                                  nd, gkeys, sm, wave * QS + s, K,
                                                                                  upd[s], stats, sp, emb, qv[s],
                                                                                  &kth[s], share);
@@ -1723,7 +1734,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
         constexpr int s = decltype(sc)::value;
         if constexpr (!CENT) {
           if (nfired[s] > cur[s].head || cur[s].rem != 0u)
-            thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS, !CENT>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s],
+            thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS, !CENT, W>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s],
                                              qcnt[s], kept[s], cur[s], nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s],
                                              stats, sp, emb, qv[s], &kth[s], share);
         }
@@ -2137,7 +2148,8 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     (void)dbg;
 #endif
     // counter (STATS) builds of the first pass exist in the base geometry only
-    const int geo = stats_first ? kGeoBase : first_geometry(nd, max_q);
+    // counter builds run the base geometry, or with dbg bit 18 the product's own (centroid) geometry
+    const int geo = stats_first && !(dbg & (1 << 18)) ? kGeoBase : first_geometry(nd, max_q);
     const bool wide = geo == kGeoWide;
     int rt, P;
     host_plan_for(max_q, nd, geo, rt, P);
@@ -2169,7 +2181,16 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     } else
 #endif
 #ifdef FWAV_DEBUG_API
-    if (stats_first) {
+    if (stats_first && geo == kGeoCent) {
+      if (mode1 == kModeHL)
+        k_sim_topk_f16<k16Cap, true, kModeHL, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
+            emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P,
+            dbg & 65535, stats, sp, ties);
+      else
+        k_sim_topk_f16<k16Cap, true, kModeS16, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
+            emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P,
+            dbg & 65535, stats, sp, ties);
+    } else if (stats_first) {
       if (mode1 == kModeHL) FWAV_FIRST(kModeHL, true, dbg & 65535, stats);
       else FWAV_FIRST(kModeS16, true, dbg & 65535, stats);
     } else

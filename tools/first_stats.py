@@ -1,6 +1,6 @@
 """Counters of the fp16 search's first pass (STATS build of the kernel: replayed chunks, firing tiles, appends,
 compactions, time shares) on cfg2 for the first AB_NQ queries (tools only).
-usage: AB_NQ=41344 python tools/first_stats.py"""
+usage: AB_NQ=41344 python tools/first_stats.py   (AB_DBG=262144: the product's centroid geometry instead of the base)"""
 import os as _os_dbg
 _os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
@@ -47,7 +47,7 @@ for rep in range(2):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
-         64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 0, stats.data_ptr(), st)
+         64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), int(os.environ.get("AB_DBG", "0")), stats.data_ptr(), st)
     e1.record()
     torch.cuda.synchronize()
     sv = stats.cpu().tolist()
@@ -56,4 +56,6 @@ for rep in range(2):
     print(f"rep {rep}: {e0.elapsed_time(e1):.2f} ms (STATS build); per query set of 32: replayed chunks "
           f"{sv[0] / qsets:.0f}, firing tiles {sv[1] / qsets:.0f}; per query: appends {sv[2] / nq:.1f}, compactions "
           f"{sv[3] / nq:.2f}; shares: barrier {sv[7] / tot:.3f} streaming {sv[9] / tot:.3f} replays {sv[4] / tot:.3f} "
-          f"(appends {sv[10] / tot:.3f}, fragment waits {sv[11] / tot:.3f}) final {sv[8] / tot:.3f}", flush=True)
+          f"(appends {sv[10] / tot:.3f}, fragment waits {sv[11] / tot:.3f}) final {sv[8] / tot:.3f}; own chunk DMA "
+          f"wait {sv[12] / tot:.3f}, compactions {sv[5] / tot:.3f}; centroid: level 1 {sv[13] / tot:.3f}, level-2 pairs "
+          f"per query set {sv[14] / qsets:.0f}", flush=True)
