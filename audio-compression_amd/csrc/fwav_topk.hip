@@ -1964,7 +1964,8 @@ constexpr int kWideW = 16, kWideG = 8;
 constexpr int kWideQB = 32 * kWideW;
 constexpr int kCentQS = FWAV_TOPK_CENT > 0 ? FWAV_TOPK_CENT : 4, kCentW = FWAV_TOPK_CW, kCentG = FWAV_TOPK_CG;
 constexpr int kCentQB = 32 * kCentW * kCentQS;
-constexpr int kCentWideQB = 32 * kWideW * kCentQS;  // the centroid filter in the wide geometry (16 waves, 8 chunks)
+constexpr int kCentWideQS = 2;  // the centroid filter in the wide geometry: 16 waves × 2 sets, 8 chunks per barrier
+constexpr int kCentWideQB = 32 * kWideW * kCentWideQS;
 #ifdef FWAV_DEBUG_API
 static int g_wide = -1;  // fwav_debug_topk_geometry (debug library only): force base / wide / centroid
 #else
@@ -2017,7 +2018,7 @@ static void topk_device_slots(int geo, int& cus, int& per_cu) {
                   &w, k_sim_topk_f16<k16Cap, false, kModeS16, kCentW, kCentG, kCentQS, true>, 64 * kCentW, 0)
         : geo == kGeoCentWide
             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                  &w, k_sim_topk_f16<k16Cap, false, kModeHL, kWideW, kWideG, kCentQS, true>, 64 * kWideW, 0)
+                  &w, k_sim_topk_f16<k16Cap, false, kModeHL, kWideW, kWideG, kCentWideQS, true>, 64 * kWideW, 0)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, k_sim_topk_f16<k16Cap, false, kModeS16>, 64 * k16Waves,
                                                            0);
     if (!(hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && occ == hipSuccess &&
@@ -2168,7 +2169,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
       sp, ties)
 #define FWAV_FIRST_CENTW(MODE_)                                                                                  \
-  k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG, kCentQS, true><<<pl.items(), 64 * kWideW, 0, st>>>(        \
+  k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG, kCentWideQS, true><<<pl.items(), 64 * kWideW, 0, st>>>(    \
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
       sp, ties)
 #define FWAV_FIRST_CENT(MODE_)                                                                                   \
@@ -2386,7 +2387,7 @@ int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t*
                  "fwav_debug_topk_plan_cover: bad args");
   const int geo = wide;  // 0 base, 1 wide, 2 centroid, 3 centroid wide
   const int W = (geo == kGeoWide || geo == kGeoCentWide) ? kWideW : (geo == kGeoCent ? kCentW : k16Waves);
-  const int sets = (geo == kGeoCent || geo == kGeoCentWide) ? kCentQS : k16Sets, qb = 32 * W * sets;
+  const int sets = geo == kGeoCent ? kCentQS : (geo == kGeoCentWide ? kCentWideQS : k16Sets), qb = 32 * W * sets;
   const TopkPlan pl = make_plan(n, rt, pieces, qb);
   *items = pl.items();
   for (int64_t it = 0; it < pl.items(); ++it) {
