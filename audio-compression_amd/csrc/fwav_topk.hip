@@ -467,6 +467,9 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_CB
 #define FWAV_TOPK_CB 4  // centroid level 2: (tile, set) pairs in flight together (2: +0.5 % at cfg2)
 #endif
+#ifndef FWAV_TOPK_CDMA
+#define FWAV_TOPK_CDMA 0  // centroid geometry: the next group's DMA at the group top (0), after level 1 (1) / level 2 (2)
+#endif
 #ifndef FWAV_TOPK_CSHARE
 #define FWAV_TOPK_CSHARE 1  // centroid geometry: read the pieces' shared limits every group (else at window ends)
 #endif
@@ -1597,7 +1600,9 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     }
     const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(7, t_b1 - t_b0);
-    if (g + 1 < ngroups) issue_group(g + 1);
+    // CENT, FWAV_TOPK_CDMA = 1 / 2: the next group's DMA issued after level 1 / after level 2 instead (a compaction's
+    // vmcnt(0) then need not wait for it)
+    if (g + 1 < ngroups && (!CENT || FWAV_TOPK_CDMA == 0)) issue_group(g + 1);
     if (ABL && (dbg & 2)) continue;
     if (CENT && FWAV_TOPK_CSHARE && share != nullptr) {
       // CENT: the pieces' shared limits every group (a filter threshold that rises sooner skips more level-2 work)
@@ -1630,6 +1635,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           for (int s = 0; s < QS; ++s) pend[s] |= pc[s] << (8 * (c - cg));
         }
       }
+      if (FWAV_TOPK_CDMA == 1 && g + 1 < ngroups) issue_group(g + 1);
       if (STATS) {
         stat_add(13, __builtin_amdgcn_s_memrealtime() - t_l1);
         unsigned long long np = 0;
@@ -1706,6 +1712,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           }
         }
       });
+      if (FWAV_TOPK_CDMA == 2 && g + 1 < ngroups) issue_group(g + 1);
     } else if (ABL && (dbg & (512 | 1024)) && c_end - cg == G) {
       // ablations 512: fold without ballots, 1024: MFMA without fold (outputs invalid)
       if (dbg & 1024)
