@@ -467,9 +467,6 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_CB
 #define FWAV_TOPK_CB 4  // centroid level 2: (tile, set) pairs in flight together (2: +0.5 % at cfg2)
 #endif
-#ifndef FWAV_TOPK_PREFIX
-#define FWAV_TOPK_PREFIX 1  // band selects skip the key bits every key shares
-#endif
 #ifndef FWAV_TOPK_CDMA
 #define FWAV_TOPK_CDMA 0  // centroid geometry: the next group's DMA at the group top (0), after level 1 (1) / level 2 (2)
 #endif
@@ -660,53 +657,6 @@ __device__ __forceinline__ int two_end_slot(int e, int n0) {
   return e < n0 ? e : C - 1 - (e - n0);
 }
 
-// The greedy bitwise select of the band limit: the largest T on the grid of key bits ≥ LO with at least K of the
-// keys hi[] ≥ T (0 = empty slot; n ≥ K real keys).  The bits above the highest bit where the largest and the smallest
-// real key differ are common to every key, so the greedy steps over them are decided in advance (a set prefix bit
-// always passes, a clear one never): the loop runs only over the bits below it (S16 bands: ≈ 11 of 20 steps).
-template <int E, int LO>
-__device__ __forceinline__ uint32_t band_select(const uint32_t (&hi)[E], int K) {
-  uint32_t mn = 0xffffffffu, mx = 0u;
-#pragma unroll
-  for (int j = 0; j < E; ++j) {
-    mn = hi[j] != 0u ? min(mn, hi[j]) : mn;
-    mx = max(mx, hi[j]);
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-  }
-  mn = __builtin_amdgcn_readfirstlane(mn);
-  mx = __builtin_amdgcn_readfirstlane(mx);
-  const uint32_t diff = mn ^ mx;
-  const int top = diff == 0u ? LO - 1 : 31 - __builtin_clz(diff);  // highest differing bit
-  uint32_t T = top >= 31 ? 0u : (mx & ~((2u << top) - 1u));        // the common prefix above it
-  if (top < LO) return T & ~((1u << LO) - 1u);
-  for (int bit = top; bit >= LO; --bit) {
-    const uint32_t Tc = T | (1u << bit);
-    int c = 0;
-#pragma unroll
-    for (int j = 0; j < E; ++j) c += __popcll(__ballot(hi[j] >= Tc));
-    if (c >= K) T = Tc;
-  }
-  return T;
-}
-
-// The same select over every bit (A/B reference: FWAV_TOPK_PREFIX=0).
-template <int E, int LO>
-__device__ __forceinline__ uint32_t band_select_full(const uint32_t (&hi)[E], int K) {
-  uint32_t T = 0;
-  for (int bit = 31; bit >= LO; --bit) {
-    const uint32_t Tc = T | (1u << bit);
-    int c = 0;
-#pragma unroll
-    for (int j = 0; j < E; ++j) c += __popcll(__ballot(hi[j] >= Tc));
-    if (c >= K) T = Tc;
-  }
-  return T;
-}
-
 template <int C, bool HL, class SM>
 __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0, int n1, SM& sm, int ql, int K,
                                               unsigned long long* stats, int& m_out, float& lim_out) {
@@ -725,8 +675,15 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0,
   }
   float lim = -INFINITY;
   if (n >= K) {
+    uint32_t T = 0;
     // HL: full precision; S16: the top 20 key bits (S16 is needed only as a lower bound at ≈ 2^-11 resolution)
-    const uint32_t T = FWAV_TOPK_PREFIX ? band_select<E, HL ? 0 : 12>(hi, K) : band_select_full<E, HL ? 0 : 12>(hi, K);
+    for (int bit = 31; bit >= (HL ? 0 : 12); --bit) {
+      const uint32_t Tc = T | (1u << bit);
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < E; ++j) c += __popcll(__ballot(hi[j] >= Tc));
+      if (c >= K) T = Tc;
+    }
     lim = HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta;
   }
   // keep: every real entry with shl > lim, written densely in (j, lane) order
@@ -862,10 +819,14 @@ __device__ __forceinline__ void piece_band(uint64_t* __restrict__ kq, SM& sm, in
   // that the pieces still streaming and k_merge_pieces see it
   uint32_t Lk = 0u;
   if (n >= K) {
-    uint32_t hk[E];
+    uint32_t T = 0;
+    for (int bit = 31; bit >= (HL ? 0 : 12); --bit) {
+      const uint32_t Tc = T | (1u << bit);
+      int c = 0;
 #pragma unroll
-    for (int j = 0; j < E; ++j) hk[j] = (uint32_t)(v[j] >> 32);
-    const uint32_t T = FWAV_TOPK_PREFIX ? band_select<E, HL ? 0 : 12>(hk, K) : band_select_full<E, HL ? 0 : 12>(hk, K);
+      for (int j = 0; j < E; ++j) c += __popcll(__ballot((uint32_t)(v[j] >> 32) >= Tc));
+      if (c >= K) T = Tc;
+    }
     Lk = f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta);
     if (lane == 0) atomicMax(share_q, Lk);
   }
