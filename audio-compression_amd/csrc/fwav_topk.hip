@@ -467,6 +467,12 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_CB
 #define FWAV_TOPK_CB 4  // centroid level 2: (tile, set) pairs in flight together (2: +0.5 % at cfg2)
 #endif
+#ifndef FWAV_TOPK_CRING
+#define FWAV_TOPK_CRING 0  // centroid geometry: a ring of this many slots of G chunks instead of the barrier (≥ 4)
+#endif
+#ifndef FWAV_TOPK_BRING
+#define FWAV_TOPK_BRING 0  // base geometry: the same ring (≥ 4)
+#endif
 #ifndef FWAV_TOPK_CDMA
 #define FWAV_TOPK_CDMA 0  // centroid geometry: the next group's DMA at the group top (0), after level 1 (1) / level 2 (2)
 #endif
@@ -1426,8 +1432,18 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
   // ALL of the kernel's LDS is one __shared__ object: beside a second one, hipcc waits vmcnt(0) for the in-flight
   // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
+  // RING (experiment; narrow geometries, FWAV_TOPK_CRING / _BRING = NB ≥ 4 slots of G chunks): no workgroup
+  // barrier per group — each wave signals its chunk DMA landed (rdy) and the slot consumed (fin) on LDS counters, and
+  // waits only for what it needs: the group's chunks from every wave, and the slot it refills freed by every wave.
+  // Groups are prefetched PD = NB/2 ahead, so a wave may run up to PD groups ahead of the slowest one (a compaction
+  // or a window-end replay no longer stalls the other waves at once).
+  constexpr int NBR = CENT ? FWAV_TOPK_CRING : FWAV_TOPK_BRING;
+  constexpr bool RING = W <= 8 && NBR >= 4;
+  constexpr int NB = RING ? NBR : 2;
+  constexpr int PD = NB / 2;
   struct Lds {
-    u32x4 slots[2 * G][512];
+    u32x4 slots[NB * G][512];
+    uint32_t ring_rdy[NB], ring_fin[NB];
     Topk16SmemT<NG, STATS, !CENT, W> sm;
   };
   __shared__ __attribute__((aligned(16))) Lds lds_all;
@@ -1560,7 +1576,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
         // inline asm, not the builtin: hipcc would otherwise wait for this DMA (vmcnt(0)) before every ds_read
         // of the other half; completion is counted by hand at the group top
         const unsigned lds_dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(
-            (__attribute__((address_space(3))) void*)(&slots[(gg & 1) * G + j][k * 64])));
+            (__attribute__((address_space(3))) void*)(&slots[(gg % NB) * G + j][k * 64])));
         const u32x4* gsrc = src + (int64_t)c_ * 512 + k * 64 + lane;
         unsigned keep;
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -1571,7 +1587,29 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   // retire the prologue's ordinary loads (query fragments, active list) before the stream, visibly to hipcc
   // (a load still pending at the loop head is waited on, vmcnt(0), inside every chunk iteration)
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  if (ngroups > 0) issue_group(0);
+  auto ring_ctr = [&](uint32_t* p) { return (__attribute__((address_space(3))) uint32_t*)(p); };
+  // spin (wave-uniform) until an LDS counter reaches target; bounded, so that a bug cannot hang the device
+  auto ring_wait = [&](uint32_t* p, uint32_t target) {
+    for (int it = 0; it < (1 << 21); ++it) {
+      const uint32_t v = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(ring_ctr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (v >= target) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  auto ring_signal = [&](uint32_t* p) {
+    if (lane == 0) __hip_atomic_fetch_add(ring_ctr(p), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  if constexpr (RING) {
+    if (threadIdx.x < NB) {
+      lds_all.ring_rdy[threadIdx.x] = 0u;
+      lds_all.ring_fin[threadIdx.x] = 0u;
+    }
+    __syncthreads();  // (the waves without queries have exited: the barrier counts the remaining ones)
+    for (int gg = 0; gg < PD && gg < ngroups; ++gg) issue_group(gg);
+  } else if (ngroups > 0) {
+    issue_group(0);
+  }
 
   int sink = 0;     // ablation builds: keeps the MFMA / fold results of dbg 512/1024 alive
   int nfired[QS];  // wave-uniform FIFO tail: chunks recorded in sm.fired[group] so far
@@ -1584,12 +1622,28 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     cur[s] = ReplayCursor{0, 0, 0u};
   }
   for (int g = 0; g < ngroups; ++g) {
-    u32x4(*half)[512] = slots + (g & 1) * G;
+    u32x4(*half)[512] = slots + (g % NB) * G;
     const int cg = c0 + g * G;  // first chunk of group g
     const int c_end = cg + G < c1 ? cg + G : c1;
     const bool window_end =
         (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
     const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+    if constexpr (RING) {
+      if (g >= 1) {  // done with group g − 1's slot (its ds_reads retired)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ring_signal(&lds_all.ring_fin[(g - 1) % NB]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's chunk DMA of group g (and up to g + PD − 1)
+      if (STATS) stat_add(12, __builtin_amdgcn_s_memrealtime() - t_b0);
+      ring_signal(&lds_all.ring_rdy[g % NB]);
+      ring_wait(&lds_all.ring_rdy[g % NB], (uint32_t)(Wact * (g / NB + 1)));
+      if (g + PD < ngroups) {  // group g + PD into the slot of group g + PD − NB, once every wave has left it
+        if (g + PD - NB >= 0)
+          ring_wait(&lds_all.ring_fin[(g + PD - NB) % NB], (uint32_t)(Wact * ((g + PD - NB) / NB + 1)));
+        issue_group(g + PD);
+      }
+      asm volatile("" ::: "memory");
+    } else
     // RAW: own DMA of group g retired, then every wave's (barrier).  WAR: the other half was last read in
     // iteration g−1, whose ds_reads were all consumed before its waves reached this barrier.
     if (!(ABL && (dbg & 256))) {  // ablation 256: no group barrier (LDS races; timing only)
@@ -1602,7 +1656,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     if (STATS) stat_add(7, t_b1 - t_b0);
     // CENT, FWAV_TOPK_CDMA = 1 / 2: the next group's DMA issued after level 1 / after level 2 instead (a compaction's
     // vmcnt(0) then need not wait for it)
-    if (g + 1 < ngroups && (!CENT || FWAV_TOPK_CDMA == 0)) issue_group(g + 1);
+    if (!RING && g + 1 < ngroups && (!CENT || FWAV_TOPK_CDMA == 0)) issue_group(g + 1);
     if (ABL && (dbg & 2)) continue;
     if (CENT && FWAV_TOPK_CSHARE && share != nullptr) {
       // CENT: the pieces' shared limits every group (a filter threshold that rises sooner skips more level-2 work)
@@ -1635,7 +1689,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           for (int s = 0; s < QS; ++s) pend[s] |= pc[s] << (8 * (c - cg));
         }
       }
-      if (FWAV_TOPK_CDMA == 1 && g + 1 < ngroups) issue_group(g + 1);
+      if (!RING && FWAV_TOPK_CDMA == 1 && g + 1 < ngroups) issue_group(g + 1);
       if (STATS) {
         stat_add(13, __builtin_amdgcn_s_memrealtime() - t_l1);
         unsigned long long np = 0;
@@ -1712,7 +1766,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           }
         }
       });
-      if (FWAV_TOPK_CDMA == 2 && g + 1 < ngroups) issue_group(g + 1);
+      if (!RING && FWAV_TOPK_CDMA == 2 && g + 1 < ngroups) issue_group(g + 1);
     } else if (ABL && (dbg & (512 | 1024)) && c_end - cg == G) {
       // ablations 512: fold without ballots, 1024: MFMA without fold (outputs invalid)
       if (dbg & 1024)
