@@ -470,6 +470,9 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_CRING
 #define FWAV_TOPK_CRING 0  // centroid geometry: a ring of this many slots of G chunks instead of the barrier (≥ 4)
 #endif
+#ifndef FWAV_TOPK_CVACC
+#define FWAV_TOPK_CVACC 1  // centroid level 1: firing tiles accumulated per lane in a VGPR (else scalar masks per set)
+#endif
 #ifndef FWAV_TOPK_BRING
 #define FWAV_TOPK_BRING 0  // base geometry: the same ring (≥ 4)
 #endif
@@ -1387,6 +1390,24 @@ __device__ __forceinline__ void cent_level1(const _Float16* __restrict__ lda0, h
 #pragma unroll
   for (int i = 0; i < 3 && i < NT; ++i) a[i] = rd(i);
   acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], bc, floatx16{}, 0, 0, 0);
+if constexpr (FWAV_TOPK_CVACC && NT <= 32) {
+  // the lane's firing tiles accumulated in a VGPR (bits = 2·bits + fired, one v_addc per tile: tile i at bit NT−1−i),
+  // then OR-reduced over the lanes of each set once per group — instead of 4 scalar ops per set and tile
+  uint32_t bits = 0u;
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    if (i + 3 < NT) a[i + 3] = rd(i + 3);
+    if (i + 1 < NT) acc[i + 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i + 1], bc, floatx16{}, 0, 0, 0);
+    const uint64_t m = __ballot(fold16((int)0x80000000, acc[i]) > thc);
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(bits), "=s"(co) : "v"(bits), "s"(m));
+  }
+#pragma unroll
+  for (int off = QS; off < 64; off <<= 1) bits |= (uint32_t)__shfl_xor((int)bits, off);
+#pragma unroll
+  for (int s = 0; s < QS; ++s)
+    pend[s] = (uint64_t)(__builtin_bitreverse32((uint32_t)__builtin_amdgcn_readlane((int)bits, s)) >> (32 - NT));
+} else {
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     if (i + 3 < NT) a[i + 3] = rd(i + 3);
@@ -1396,6 +1417,7 @@ __device__ __forceinline__ void cent_level1(const _Float16* __restrict__ lda0, h
     for (int s = 0; s < QS; ++s)
       if (m & cent_set_mask<QS>(s)) pend[s] |= 1ull << i;
   }
+}
 #ifdef FWAV_TOPK_CENTSTATS
   if ((threadIdx.x & 63) == 0) {
     unsigned long long np = 0;
