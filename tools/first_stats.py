@@ -36,6 +36,8 @@ ws = torch.empty(max(size_call("fwav_pool_workspace_size", sig.numel(), 2048, 8,
                  device="cuda")
 call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
      emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+if os.environ.get("AB_PLAN"):  # "rt,pieces": the work-plan override (fwav_debug_topk_plan), set before sizing
+    call("fwav_debug_topk_plan", *[int(x) for x in os.environ["AB_PLAN"].split(",")])
 nq = int(os.environ.get("AB_NQ", nr))
 active = torch.arange(nq, dtype=torch.int32, device="cuda")
 n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
