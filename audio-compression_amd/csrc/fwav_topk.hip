@@ -1863,7 +1863,15 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   if (STATS) {
     stat_add(8, __builtin_amdgcn_s_memrealtime() - t_final);
     stat_add(6, __builtin_amdgcn_s_memrealtime() - t_kernel);
-    if (gstats != nullptr && lane < kStats) atomicAdd(gstats + lane, sm.wstat[wave][lane]);
+    // [15]: per workgroup, the busiest wave's time outside the group barrier (Σ over workgroups; against the mean
+    // Σ([6] − [7]) / waves it tells a systematic per-wave imbalance from a per-group one)
+    __syncthreads();
+    if (gstats != nullptr && threadIdx.x == 0) {
+      unsigned long long mx = 0;
+      for (int w = 0; w < Wact; ++w) mx = max(mx, sm.wstat[w][6] - sm.wstat[w][7]);
+      atomicAdd(gstats + 15, mx);
+    }
+    if (gstats != nullptr && lane < kStats && lane != 15) atomicAdd(gstats + lane, sm.wstat[wave][lane]);
     // dbg 4096: workgroup timeline (start of its first wave, end of its last) at gstats[16 + 2·block]
     if (gstats != nullptr && (dbg & 4096) && lane == 0) {
       atomicMin(gstats + 16 + 2 * blockIdx.x, t_kernel);

@@ -60,4 +60,5 @@ for rep in range(2):
           f"{sv[3] / nq:.2f}; shares: barrier {sv[7] / tot:.3f} streaming {sv[9] / tot:.3f} replays {sv[4] / tot:.3f} "
           f"(appends {sv[10] / tot:.3f}, fragment waits {sv[11] / tot:.3f}) final {sv[8] / tot:.3f}; own chunk DMA "
           f"wait {sv[12] / tot:.3f}, compactions {sv[5] / tot:.3f}; centroid: level 1 {sv[13] / tot:.3f}, level-2 pairs "
-          f"per query set {sv[14] / qsets:.0f}", flush=True)
+          f"per query set {sv[14] / qsets:.0f}; busiest wave / mean wave (outside the barrier) "
+          f"{sv[15] * int(os.environ.get('AB_W', 8)) / max(sv[6] - sv[7], 1):.3f}", flush=True)
