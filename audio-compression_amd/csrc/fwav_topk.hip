@@ -470,6 +470,9 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_CRING
 #define FWAV_TOPK_CRING 0  // centroid geometry: a ring of this many slots of G chunks instead of the barrier (≥ 4)
 #endif
+#ifndef FWAV_TOPK_BSHARE
+#define FWAV_TOPK_BSHARE 0  // base geometry: read the pieces' shared limits every group too (else at window ends)
+#endif
 #ifndef FWAV_TOPK_CVACC
 #define FWAV_TOPK_CVACC 1  // centroid level 1: firing tiles accumulated per lane in a VGPR (else scalar masks per set)
 #endif
@@ -1680,7 +1683,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     // vmcnt(0) then need not wait for it)
     if (!RING && g + 1 < ngroups && (!CENT || FWAV_TOPK_CDMA == 0)) issue_group(g + 1);
     if (ABL && (dbg & 2)) continue;
-    if (CENT && FWAV_TOPK_CSHARE && share != nullptr) {
+    if (((CENT && FWAV_TOPK_CSHARE) || (!CENT && FWAV_TOPK_BSHARE)) && share != nullptr) {
       // CENT: the pieces' shared limits every group (a filter threshold that rises sooner skips more level-2 work)
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
