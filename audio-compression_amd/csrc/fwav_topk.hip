@@ -31,6 +31,7 @@
 // (score, index) keys that beat θ to the query's LDS buffer; a nearly full buffer is sorted (64-lane bitonic), cut
 // to its top K and θ set to the K-th score.  Domains stream in increasing index order, so a later domain whose
 // score equals θ can never displace an earlier one: strict '>' is exact.
+#include <type_traits>
 #include "fwav_common.h"
 #include "../../include/fwav.h"
 
@@ -469,6 +470,12 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #endif
 #ifndef FWAV_TOPK_CRING
 #define FWAV_TOPK_CRING 0  // centroid geometry: a ring of this many slots of G chunks instead of the barrier (≥ 4)
+#endif
+#ifndef FWAV_TOPK_L2M32
+#define FWAV_TOPK_L2M32 0  // centroid level 2: 32-bit tile masks when a group has ≤ 32 tiles
+#endif
+#ifndef FWAV_TOPK_APPOFF
+#define FWAV_TOPK_APPOFF 1  // appends: running byte offset and a one-op key low word (else slot arithmetic per row)
 #endif
 #ifndef FWAV_TOPK_BSHARE
 #define FWAV_TOPK_BSHARE 0  // base geometry: read the pieces' shared limits every group too (else at window ends)
@@ -1003,6 +1010,25 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
         }
       }
     }
+  } else if constexpr (FWAV_TOPK_APPOFF) {
+    // a running byte offset (one add per stored row, the store's own VGPR offset) and the key's low word as one
+    // subtraction from an opaque nd0 (the compiler otherwise derives it from dt's known low bits in two ops)
+    uint32_t off = (uint32_t)((ql * C + slot) * 8);
+    const uint32_t dstep = h ? (uint32_t)-8 : 8u;
+    uint32_t nd0o = nd0;
+    asm volatile("" : "+v"(nd0o));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (a[r] > thf) {
+        FWAV_TRACE(sm.qrow[ql], 1u, (uint32_t)dt, (uint32_t)((h << 16) | r), (uint32_t)(off / 8 - ql * C));
+        const uint32_t u = __float_as_uint(a[r]);
+        const uint32_t key = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+        const uint64_t k64 = ((uint64_t)key << 32) | (uint64_t)(nd0o - (uint32_t)((r & 3) + 8 * (r >> 2)));
+        *reinterpret_cast<uint64_t*>(kbase + off) = k64;
+        off += dstep;
+      }
+    }
+    slot = (int)(off / 8) - ql * C;
   } else {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -1278,6 +1304,8 @@ __device__ __forceinline__ void stream_group(const _Float16* __restrict__ lda0, 
   }
 }
 
+__device__ __forceinline__ int ctz_mask(uint32_t x) { return __builtin_ctz(x); }
+__device__ __forceinline__ int ctz_mask(uint64_t x) { return __builtin_ctzll(x); }
 // f(std::integral_constant<int, I>) for I = 0 .. N−1: loops over per-set register arrays with compile-time indices
 // where the body is too large for the unroller
 template <int N, int I = 0, class F>
@@ -1728,15 +1756,17 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       // memory round trip per batch, as the base geometry's replays) and appended.
       static_for<QS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        uint64_t pm = pend[s];
-        uint64_t pass = 0ull;  // HL: tiles whose s16 passes the set's stream threshold
-        while (pm != 0ull) {
+        // tile masks in 32 bits when a group has at most 32 tiles (half the scalar ops of the 64-bit bit walk)
+        using TMask = std::conditional_t<(FWAV_TOPK_L2M32 && 8 * G <= 32), uint32_t, uint64_t>;
+        TMask pm = (TMask)pend[s];
+        TMask pass = 0;  // HL: tiles whose s16 passes the set's stream threshold
+        while (pm != 0) {
           int t[kCentBatch];
           bool on[kCentBatch];
 #pragma unroll
           for (int u = 0; u < kCentBatch; ++u) {
-            on[u] = pm != 0ull;
-            t[u] = on[u] ? __builtin_ctzll(pm) : t[0];
+            on[u] = pm != 0;
+            t[u] = on[u] ? ctz_mask(pm) : t[0];
             if (on[u]) pm &= pm - 1;
           }
           half8 af[kCentBatch];
@@ -1751,7 +1781,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           for (int u = 0; u < kCentBatch; ++u) {
             if (!on[u]) break;
             if constexpr (HL) {
-              if (__ballot(fold16((int)0x80000000, acc[u]) > thi[s]) != 0ull) pass |= 1ull << t[u];
+              if (__ballot(fold16((int)0x80000000, acc[u]) > thi[s]) != 0ull) pass |= (TMask)1 << t[u];
             } else {
               const int64_t dt = (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32;
               thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT, W>, MODE>(acc[u], thf[s], qcnt[s], kept[s],
@@ -1762,13 +1792,13 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           }
         }
         if constexpr (HL) {  // shl = s16 + d_hi·q_lo + d_lo·q_hi for the passing tiles, batched
-          while (pass != 0ull) {
+          while (pass != 0) {
             int t[kReplayBatch];
             bool on[kReplayBatch];
 #pragma unroll
             for (int u = 0; u < kReplayBatch; ++u) {
-              on[u] = pass != 0ull;
-              t[u] = on[u] ? __builtin_ctzll(pass) : t[0];
+              on[u] = pass != 0;
+              t[u] = on[u] ? ctz_mask(pass) : t[0];
               if (on[u]) pass &= pass - 1;
             }
             half8 afl[kReplayBatch];
