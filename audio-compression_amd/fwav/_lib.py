@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 from . import _digest
 
@@ -82,7 +83,26 @@ _libs: dict = {}
 _active = None  # the debug library inside debug_library(), else the product library
 
 
+#: set by fwav.hipctypes, the torch-free host: the library then binds the system HIP runtime on its own
+TORCH_FREE = False
+
+
+def _one_runtime() -> None:
+    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 (same soname, libamdhip64.so.7, but
+    torch's libraries ask for it by another name), so a process that loads libfwav.so — which binds the system
+    runtime — before torch ends up with two HIP runtimes, and the second one to initialise sees no device
+    ("no ROCm-capable device is detected").  Loaded after torch, libfwav.so binds torch's runtime.  So unless the
+    caller is torch-free, torch is imported first."""
+    if TORCH_FREE or "torch" in sys.modules:
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load(path: str, sigs: dict) -> C.CDLL:
+    _one_runtime()
     if not os.path.exists(path):
         raise FwavError(f"HIP library not built: {path} is missing (run __graft_entry__.build())")
     dll = C.CDLL(path)

@@ -13,8 +13,11 @@ import ctypes as C
 import numpy as np
 
 from . import geometry
+from . import _lib
 from ._lib import FwavError, call, size_call
 from .nporder import blas_threads, numpy_topk_row, zero_query_candidates
+
+_lib.TORCH_FREE = True  # this host never imports torch: libfwav.so binds the system HIP runtime
 
 _HIP = None
 H2D, D2H = 1, 2
