@@ -195,3 +195,38 @@ def test_work_plan_covers_every_query(lib, n, rt, pieces, wide):
         split = (g % nb) >= nb - R
         expect[split] = pieces
     assert np.array_equal(count, expect)
+
+
+_MAPS = r"""
+import sys
+sys.path[:0] = [{root!r}, {pkg!r}]
+{pre}
+from fwav import _lib
+_lib.product_lib()
+hip = sorted({{l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l}})
+print("HIP", "torch" in sys.modules, hip)
+"""
+
+
+@pytest.mark.parametrize("pre", ["", "from fwav import hipctypes"])
+def test_one_hip_runtime_per_process(lib, pre):
+    """libfwav.so loaded with no torch imported yet must still leave ONE HIP runtime in the process: PyTorch-ROCm
+    ships its own libamdhip64, and a library that bound the system one first left torch a second runtime that saw no
+    device.  The torch-free host (fwav.hipctypes) binds the system runtime and never imports torch."""
+    import subprocess
+    import sys
+    code = _MAPS.format(root=ROOT, pkg=os.path.join(ROOT, "audio-compression_amd"), pre=pre)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
+    line = [x for x in out.stdout.splitlines() if x.startswith("HIP")]
+    assert out.returncode == 0 and line, out.stderr[-2000:]
+    torch_loaded = line[0].split()[1] == "True"
+    hip = eval(line[0].split(" ", 2)[2])
+    assert len(hip) == 1, hip
+    if pre:
+        assert not torch_loaded and "/torch/" not in hip[0]
+    else:
+        try:
+            import torch  # noqa: F401
+            assert torch_loaded and "/torch/" in hip[0]
+        except ImportError:
+            pass
