@@ -67,6 +67,21 @@ def test_debug_library_split(lib):
     assert lib.lib() is lib.product_lib()
 
 
+@pytest.mark.parametrize("switch", ["FWAV_TOPK_ABL=1", "FWAV_TOPK_EXTSEED", "FWAV_TOPK_DEBUG", "FWAV_TOPK_CENTSTATS",
+                                    "FWAV_TOPK_CENT_L2OFF", "FWAV_TOPK_PADLDS=0"])
+def test_product_build_refuses_experiment_switches(switch):
+    """An experiment code path compiled without -DFWAV_DEBUG_API stops the build (#error): the product library can
+    carry none of them (libfwav_debug.so, built with -DFWAV_DEBUG_API, is where they compile)."""
+    import shutil
+    import subprocess
+    if shutil.which("hipcc") is None:
+        pytest.skip("hipcc not available")
+    src = os.path.join(ROOT, "audio-compression_amd", "csrc", "fwav_topk.hip")
+    cmd = ["hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only", f"-D{switch}", src]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and "experiment switches build the debug library only" in out.stderr
+
+
 def test_error_codes_without_gpu(lib):
     L = lib.lib()
     assert L.fwav_abi_version() == 4
