@@ -466,7 +466,7 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #define FWAV_TOPK_CWPE 4
 #endif
 #ifndef FWAV_TOPK_CB
-#define FWAV_TOPK_CB 4  // centroid level 2: (tile, set) pairs in flight together (2: +0.5 % at cfg2)
+#define FWAV_TOPK_CB 2  // centroid level 2: (tile, set) pairs in flight together (4: +0.8 % cfg2, +10 % at 82,688 queries; 6, 8: spills)
 #endif
 #ifndef FWAV_TOPK_CRING
 #define FWAV_TOPK_CRING 0  // centroid geometry: a ring of this many slots of G chunks instead of the barrier (≥ 4)
