@@ -339,7 +339,8 @@ __global__ __launch_bounds__(64 * kAffWaves) void k_affine_batch(const float* __
 // that cannot change the match when every member of G — the search records the ones left out — fits strictly worse
 // (both orientations) than the best candidate outside G, whose slot is then the minimum whatever the choice.  Queries
 // that fail either test, and K-th place ties whose group the search could not collect (or all of them with
-// exact_sets: the candidate sets themselves are then the reference's), go to `resolve` for the host (fwav.ties:
+// exact_sets == 1: the candidate sets themselves are then the reference's; every listed query with exact_sets == 2:
+// the whole candidate rows, order included, are then the reference's), go to `resolve` for the host (fwav.ties:
 // exact score rows + numpy's own calls).  One wave per listed query, K ≤ 64 (lane c ↔ position c); for K > 64 every
 // listed query is resolved.
 __device__ __forceinline__ bool same_err(float a, float b) { return (a != a && b != b) || a == b; }
@@ -406,7 +407,7 @@ __global__ __launch_bounds__(256) void k_tie_check(const float* __restrict__ ran
   const int32_t row = ent >> 1;
   const bool boundary = (ent & 1) != 0;
   const int ng = boundary ? rec[1] : 0;  // tied domains left out of the K (−1: group not collected)
-  bool dep = K > 64 || (boundary && (exact_sets || ng < 0));
+  bool dep = K > 64 || exact_sets >= 2 || (boundary && (exact_sets || ng < 0));
   if (!dep) {
     const int n = RS > 0 ? RS : rs;
     const bool has = lane < K;

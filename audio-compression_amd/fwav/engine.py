@@ -27,6 +27,8 @@ from .nporder import zero_query_candidates  # noqa: F401  (Q11 rows; re-exported
 from ._lib import FwavError, call, size_call
 
 F32 = np.float32
+#: tie_order → fwav_tie_check's exact_sets argument ("index" never calls it)
+TIE_MODES = {"numpy": 0, "numpy_sets": 1, "numpy_rows": 2, "index": -1}
 
 
 from . import geometry  # noqa: E402,F401  range_size, domain_step (fractal.py:1070-1071)
@@ -198,7 +200,9 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     fwav.ties.blas_threads).  ``tie_order="numpy"`` re-ranks the rows whose match depends on the order of exactly
     equal scores with numpy's own calls, as the reference does (one host synchronisation to read the count), so every
     match tuple is the reference's; ``"numpy_sets"`` also re-ranks every row with a tie at the K-th place, so that
-    the candidate sets are the reference's too; ``"index"`` keeps the device's (score desc, index asc) order (no
+    the candidate sets are the reference's too; ``"numpy_rows"`` re-ranks every row with any exact tie in its top K + 1,
+    so that every candidate row, order included, is the reference's (a parity mode: thousands of host rows at cfg2);
+    ``"index"`` keeps the device's (score desc, index asc) order (no
     synchronisation).  ``defer_ties=True`` hands that host step to a background thread (its device work on a side
     stream, after this call's kernels) and returns at once: the outputs are final after ``result.wait()``, so a
     stream of calls overlaps one call's host ranking with the next call's search.  Without deferral, a large search
@@ -223,9 +227,10 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
     lo32 = F32(energy_thresh * 0.5)
     if k > size_call("fwav_topk_max_k"):
         raise ValueError(f"top_k={k} > {size_call('fwav_topk_max_k')} is not supported by the HIP search")
-    if tie_order not in ("numpy", "numpy_sets", "index"):
+    if tie_order not in TIE_MODES:
         raise ValueError("tie_order must be 'numpy' (the reference's order of exactly tied scores wherever it decides a"
-                         " match), 'numpy_sets' (and wherever it decides a candidate set) or 'index'")
+                         " match), 'numpy_sets' (and wherever it decides a candidate set), 'numpy_rows' (and wherever it"
+                         " decides a candidate row's order) or 'index'")
     threads = _ties.blas_threads() if blas_threads is None else int(blas_threads)
     _mark(events, "voiced_ranges")
     ranges = _voiced_ranges(sig, n, rs, frame, thr32, lo32, st)
@@ -310,7 +315,7 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
             _mark(events, "ties")
             resolve = torch.empty(m + 1, dtype=torch.int32, device=dev)
             call("fwav_tie_check", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, emb.data_ptr(), lo,
-                 threads, ties.data_ptr(), m, int(tie_order == "numpy_sets"), resolve.data_ptr(), st)
+                 threads, ties.data_ptr(), m, TIE_MODES[tie_order], resolve.data_ptr(), st)
 
             def finish(stream_id):
                 counts = torch.stack([ties[0], resolve[0]]).cpu()
@@ -414,7 +419,7 @@ def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb1
              cand.data_ptr(), ties.data_ptr(), wsk.data_ptr(), wk, st)
         resolve = torch.empty(mq + 1, dtype=torch.int32, device=dev)
         call("fwav_tie_check", rsh.data_ptr(), m, rs, cand.data_ptr(), k, pool.data_ptr(), nd, emb.data_ptr(), lo,
-             threads, ties.data_ptr(), mq, int(tie_order == "numpy_sets"), resolve.data_ptr(), st)
+             threads, ties.data_ptr(), mq, TIE_MODES[tie_order], resolve.data_ptr(), st)
         counts = torch.stack([ties[0], resolve[0]]).cpu()
         if _ties._TRACE:
             import time

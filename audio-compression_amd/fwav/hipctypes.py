@@ -138,9 +138,10 @@ def compress(signal: np.ndarray, tile_size: int, top_k: int, energy_thresh: floa
     reference's ValueErrors (empty input; more ranges than domains, quirk Q9), else a dict of host arrays: idx, s, o,
     sym, err (the match tuples), pool f32[nd, rs], emb f32[nd, 16], cand i32[nr, K], n_ranges, range_size,
     domain_step, n_domains, n_ties, n_resolved.  ``tie_order`` as fwav.engine.compress_device ("numpy",
-    "numpy_sets" or "index")."""
-    if tie_order not in ("numpy", "numpy_sets", "index"):
-        raise ValueError("tie_order must be 'numpy', 'numpy_sets' or 'index'")
+    "numpy_sets", "numpy_rows" or "index")."""
+    modes = {"numpy": 0, "numpy_sets": 1, "numpy_rows": 2, "index": -1}  # → fwav_tie_check's exact_sets
+    if tie_order not in modes:
+        raise ValueError("tie_order must be 'numpy', 'numpy_sets', 'numpy_rows' or 'index'")
     sig = np.ascontiguousarray(signal, np.float32).reshape(-1)
     n = sig.size
     if n == 0:
@@ -193,7 +194,7 @@ def compress(signal: np.ndarray, tile_size: int, top_k: int, energy_thresh: floa
     if tie_order != "index":
         d_res = DeviceBuffer(4 * (nr + 1))
         call("fwav_tie_check", d_ranges.value, nr, rs, d_cand.value, k, d_pool.value, nd, d_emb.value, 0, T,
-             d_ties.value, nr, int(tie_order == "numpy_sets"), d_res.value, None)
+             d_ties.value, nr, modes[tie_order], d_res.value, None)
         n_ties = int(_i32(d_ties, 1)[0])
         res = _i32(d_res, 1 + nr)
         n_res = int(res[0])

@@ -136,7 +136,8 @@ int fwav_affine(const float* ranges, int64_t n_ranges, int range_size, const int
  * reference's numpy tie order could change its match (fractal.py:816-824) — equal scores inside the top K when two
  * candidates of one run of equal scores both attain the minimum error; a tie at the K-th place when some member of
  * the K-th score's group (in the K or left out) fits no worse than the best candidate outside it, or when the group
- * was not collected; with exact_sets != 0 every K-th place tie (the candidate sets are then the reference's too).
+ * was not collected; with exact_sets == 1 every K-th place tie (the candidate sets are then the reference's too), with
+ * exact_sets == 2 every listed query (whole candidate rows, order included, are then the reference's).
  * resolve (device int32[1 + max_ties]): resolve[0] = count, resolve[1 + j] = local row to resolve on the host
  * (fwav.ties.resolve_rows: exact score rows, numpy's argpartition/argsort, fwav_affine on those rows). */
 int fwav_tie_check(const float* ranges, int64_t n_ranges, int range_size, const int32_t* cand, int k,

@@ -364,57 +364,110 @@ def fma_f32(p: np.ndarray, c: np.ndarray) -> np.ndarray:
 SGEMV_GAP = 8e-6
 
 
+def reference_row_scores(emb: np.ndarray, q: np.ndarray, threads: int, chunk: int = 1 << 23) -> np.ndarray:
+    """One whole score row ``domain_embs @ q`` (fractal.py:537) in the reference's order.  When ``threads`` is this
+    process's OpenBLAS thread count, numpy's own call IS the reference's computation (the restatement below is pinned
+    bit for bit against it: tests/test_oracle_golden.py::test_sgemv_thread_split_pinned_against_numpy), and takes
+    0.1 s instead of 4 s for a 6.6 M-domain row; otherwise the restatement, in column chunks (bounded memory)."""
+    E = np.asarray(emb, F32)
+    q = np.asarray(q, F32)
+    nd = len(E)
+    if int(threads) == blas_threads():
+        return E @ q
+    out = np.empty(nd, F32)
+    for a in range(0, nd, chunk):
+        cols = np.arange(a, min(nd, a + chunk))
+        out[a:a + len(cols)] = sgemv_scores(E[a:a + len(cols)], q[None, :], sgemv_col_kind(cols, nd, threads))[0]
+    return out
+
+
+def topk_rows(emb: np.ndarray, qrows, k: int, threads: int, chunk: int = 512, row_scores=None):
+    """The reference's candidate rows (fractal.py:535-552) for the queries emb[qrows] (quirk Q1: query i is domain row
+    i), none of them pruned.  Rows whose top K + 1 scores are all distinct are decided by the scores alone (score
+    desc; the K-th beats the (K+1)-th); a row with exactly equal scores among its top K + 1 — and every all-zero query
+    (quirk Q11) — is scored in full and handed to numpy's own argpartition/argsort (numpy_topk_row), whose tie order
+    the reference inherits.  ``row_scores(q)``: the whole reference-order score row of query vector q (default: the
+    restatement for ``threads``; reference_row_scores).  Returns (cand i32[n, k] −1-padded, kth f32[n], k1th f32[n],
+    tied bool[n]: an exact tie among the top K + 1 — every all-zero query counts as tied)."""
+    E = np.asarray(emb, F32)
+    nd = E.shape[0]
+    qrows = np.asarray(qrows, np.int64)
+    n = len(qrows)
+    cand = np.full((n, k), -1, np.int32)
+    kth = np.full(n, np.nan, F32)
+    k1th = np.full(n, np.nan, F32)
+    tied = np.zeros(n, bool)
+    kk = min(k, nd)
+    zero = np.all(E[qrows] == 0, axis=1) if n else np.zeros(0, bool)
+    if zero.any():
+        cand[zero] = zero_query_candidates(nd, k)
+        kth[zero] = 0
+        k1th[zero] = 0
+        tied[zero] = True
+    act = np.nonzero(~zero)[0]
+    kind_all = None
+    for s in range(0, len(act), chunk):
+        pos = act[s:s + chunk]
+        # BLAS scores (another summation order: within SGEMV_GAP of the sgemv order) pick a superset of every
+        # domain that can be in the exact top K + 1; the superset is then scored in the sgemv order and selected exactly
+        fast = E[qrows[pos]] @ E.T
+        if kk < nd:
+            # the (K+1)-th BLAS score — of every stride-th column on large tables: a subset's (K+1)-th is at most the
+            # whole row's, so the superset below still holds the exact top K + 1 (a few hundred columns wider)
+            stride = max(1, nd // (1 << 20))
+            sub = fast[:, ::stride] if stride > 1 else fast
+            Tf = -np.partition(-sub, kk, axis=1)[:, kk] if sub.shape[1] > kk else sub.min(axis=1)
+            del sub
+        else:
+            Tf = fast.min(axis=1)
+        for j, p in enumerate(pos):
+            q = E[qrows[p]]
+            sup = np.nonzero(fast[j] >= Tf[j] - SGEMV_GAP)[0]
+            ex = sgemv_scores(E[sup], q[None, :], sgemv_col_kind(sup, nd, threads))[0]
+            o = np.lexsort((sup, -ex))  # (score desc, index asc)
+            top = ex[o[:kk + 1]]
+            if np.any(top[1:] == top[:-1]):
+                tied[p] = True
+                if row_scores is not None:
+                    full = row_scores(q)
+                else:
+                    if kind_all is None:
+                        kind_all = sgemv_col_kind(np.arange(nd), nd, threads)
+                    full = sgemv_scores(E, q[None, :], kind_all)[0]
+                cand[p] = numpy_topk_row(full, k)
+            else:
+                cand[p, :kk] = sup[o[:kk]]
+            kth[p] = ex[o[kk - 1]]
+            if kk < nd:
+                k1th[p] = ex[o[kk]]
+        del fast
+    return cand, kth, k1th, tied
+
+
 def topk_candidates(emb: np.ndarray, n_ranges: int, k: int, pruned: np.ndarray, chunk: int = 512,
-                    threads: int | None = None, stats: dict | None = None):
-    """cpu_worker + range_candidates_from_embedding_emb + pad_candidates (fractal.py:556-632, 535-552).
-    Query for range i is domain-embedding row i (quirk Q1, fractal.py:1190-1195).  Scores in float32 in the
-    reference's sgemv order (sgemv_scores, column kinds for `threads` OpenBLAS threads; default: this process's).
-    Rows whose top K + 1 scores are all distinct are decided by the scores alone (score desc; the K-th beats the
-    (K+1)-th); a row with exactly equal scores among its top K + 1 — and every all-zero query (quirk Q11) — is
-    scored in full and handed to numpy's own argpartition/argsort (numpy_topk_row), whose tie order the reference
-    inherits.  Returns (cand i32[nr, k] −1-padded, kth f32[nr], k1th f32[nr]); stats['ties'] counts tied rows."""
+                    threads: int | None = None, stats: dict | None = None, rows=None, row_scores=None):
+    """cpu_worker + range_candidates_from_embedding_emb + pad_candidates (fractal.py:556-632, 535-552): the energy
+    prune (pruned rows stay all −1, :602) and topk_rows for every other range — or only for ``rows``.  Scores in
+    float32 in the reference's sgemv order for ``threads`` OpenBLAS threads (default: this process's).  Returns
+    (cand i32[nr, k] −1-padded, kth f32[nr], k1th f32[nr]); stats['ties'] counts the rows with an exact tie in
+    their top K + 1 (all-zero queries aside) and stats['tie_rows'] lists them."""
     nd = emb.shape[0]
     threads = blas_threads() if threads is None else int(threads)
     cand = np.full((n_ranges, k), -1, np.int32)
     kth = np.full(n_ranges, np.nan, F32)
     k1th = np.full(n_ranges, np.nan, F32)
-    zero = np.all(emb[:n_ranges] == 0, axis=1) & ~pruned[:n_ranges]
-    if zero.any():
-        cand[zero] = zero_query_candidates(nd, k)
-        kth[zero] = 0
-        k1th[zero] = 0
-    act = np.nonzero(~pruned[:n_ranges] & ~zero)[0]
-    kk = min(k, nd)
-    E = np.asarray(emb, F32)
-    kind_all = None
-    n_ties = 0
-    for s in range(0, len(act), chunk):
-        rows = act[s:s + chunk]
-        # BLAS scores (another summation order: within SGEMV_GAP of the sgemv order) pick a superset of every
-        # domain that can be in the exact top K + 1; the superset is then scored in the sgemv order and selected exactly
-        fast = E[rows] @ E.T
-        if kk < nd:
-            part = -np.partition(-fast, kk, axis=1)
-            Tf = part[:, kk]      # the (K+1)-th BLAS score
-        else:
-            Tf = fast.min(axis=1)
-        for j, r in enumerate(rows):
-            sup = np.nonzero(fast[j] >= Tf[j] - SGEMV_GAP)[0]
-            ex = sgemv_scores(E[sup], E[r][None, :], sgemv_col_kind(sup, nd, threads))[0]
-            o = np.lexsort((sup, -ex))  # (score desc, index asc)
-            top = ex[o[:kk + 1]]
-            if np.any(top[1:] == top[:-1]):
-                n_ties += 1
-                if kind_all is None:
-                    kind_all = sgemv_col_kind(np.arange(nd), nd, threads)
-                cand[r] = numpy_topk_row(sgemv_scores(E, E[r][None, :], kind_all)[0], k)
-            else:
-                cand[r, :kk] = sup[o[:kk]]
-            kth[r] = ex[o[kk - 1]]
-            if kk < nd:
-                k1th[r] = ex[o[kk]]
+    want = np.zeros(n_ranges, bool)
+    if rows is None:
+        want[:] = True
+    else:
+        want[np.asarray(rows, np.int64)] = True
+    act = np.nonzero(want & ~pruned[:n_ranges])[0]
+    c, a, b, tied = topk_rows(emb, act, k, threads, chunk=chunk, row_scores=row_scores)
+    cand[act], kth[act], k1th[act] = c, a, b
     if stats is not None:
-        stats["ties"] = n_ties
+        zero = np.all(np.asarray(emb)[act] == 0, axis=1) if len(act) else np.zeros(0, bool)
+        stats["tie_rows"] = act[tied & ~zero].tolist()
+        stats["ties"] = len(stats["tie_rows"])
     return cand, kth, k1th
 
 

@@ -24,6 +24,7 @@ torch = pytest.importorskip("torch")
 from fwav import engine, synth, ties  # noqa: E402
 from fwav._lib import call  # noqa: E402
 from oracle import fractal_oracle as O  # noqa: E402
+from oracle_rows import check_rows  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 K = 64
@@ -112,6 +113,14 @@ def test_cfg4_one_rank_eighth_product_path():
     out = O.affine(ranges[samp], cand_h[samp], pool)
     for t, v in zip((res.idx, res.s, res.o, res.sym, res.err), out):
         assert np.array_equal(t.cpu().numpy()[samp].view(np.uint8), np.asarray(v).view(np.uint8))
+    # ≥ 64 sampled rows (and 8 of the listed tie rows) against the oracle's rows, order included where numpy's order
+    # decides it, and their match tuples = O.affine of the oracle's rows (tests/oracle_rows.py)
+    rec_rows = np.unique(rec[:, 0] >> 1)
+    orows = np.union1d(rng.choice(EIGHTH, 64, replace=False), rng.choice(rec_rows, min(8, len(rec_rows)), replace=False))
+    outs_h = tuple(t.cpu().numpy() for t in (res.idx, res.s, res.o, res.sym, res.err))
+    got_o = check_rows(emb, pool, ranges, cand_h, outs_h, orows, K, T, q_offset=lo, exact=ranked, chunk=8,
+                       label="cfg4 rank eighth")
+    assert got_o["rows"] >= 64
     print(f"cfg4 rank eighth: 16,384 rows = f32 kernel (numpy-ranked rows aside: {len(diff)}), top-K property on "
           f"8 rows, {checked} tie rows = numpy's ranking of the reference row, 4,096 tuples = oracle; "
           f"product call {wall:.2f} s")

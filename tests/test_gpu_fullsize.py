@@ -20,6 +20,7 @@ torch = pytest.importorskip("torch")
 from fwav import engine, synth, ties  # noqa: E402
 from fwav._lib import call, debug_library, size_call  # noqa: E402
 from oracle import fractal_oracle as O  # noqa: E402
+from oracle_rows import check_rows  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 K = 64
@@ -160,6 +161,28 @@ def test_cfg3_numpy_tie_order(cfg3_both):
         out = O.affine(ranges[r:r + 1], ref[None, :], pool)
         for t, v in zip((prod.idx, prod.s, prod.o, prod.sym, prod.err), out):
             assert np.array_equal(t[r:r + 1].cpu().numpy().view(np.uint8), np.asarray(v).view(np.uint8)), r
+
+
+def test_cfg3_candidate_rows_equal_oracle(cfg3_both):
+    """≥ 256 sampled active rows of the product-default cfg3 search (plus 32 of the rows it lists with exact ties)
+    against the oracle's rows in the reference's sgemv order for this process's BLAS threads (fractal.py:535-541):
+    order included wherever numpy's order decides it, and every match tuple = O.affine of the oracle's row
+    (tests/oracle_rows.py)."""
+    sig, _, prod = cfg3_both
+    T = ties.blas_threads()
+    emb = prod.emb.view(-1, 16).cpu().numpy()
+    pool = prod.pool.view(-1, 16).cpu().numpy()
+    ranges = prod.ranges.view(-1, 16).cpu().numpy()
+    cand = prod.cand.view(-1, K).cpu().numpy()
+    outs = tuple(t.cpu().numpy() for t in (prod.idx, prod.s, prod.o, prod.sym, prod.err))
+    active = np.nonzero(cand[:, 0] >= 0)[0]
+    rec = prod.ties[1:1 + engine.TIE_REC * prod.n_ties].view(-1, engine.TIE_REC).cpu().numpy()
+    listed = np.unique(rec[:, 0] >> 1)
+    rng = np.random.default_rng(33)
+    rows = np.union1d(rng.choice(active, 256, replace=False), rng.choice(listed, min(32, len(listed)), replace=False))
+    got = check_rows(emb, pool, ranges, cand, outs, rows, K, T, exact=prod.resolved.cpu().numpy(), chunk=32,
+                     label="cfg3 defaults")
+    assert got["rows"] >= 256 and got["tied"] > 0
 
 
 def test_cfg3_affine_sampled(cfg3):

@@ -158,3 +158,24 @@ def test_sgemv_thread_split_pinned_against_numpy(nd):
         assert (k1 != k8).sum() == 20
         wrong = O.sgemv_scores(e, e[qi], k1)
         assert not np.array_equal(wrong.view(np.uint32), refs[8].view(np.uint32))
+
+
+@pytest.mark.parametrize("case", ["sweep", "noise2048", "speech4096"])
+def test_full_size_row_checker_accepts_reference_rows(case):
+    """tests/oracle_rows.check_rows (the full-size GPU parity check) accepts the reference's own candidate rows and
+    match tuples, row subsets and large-table thresholds included, and rejects a row with two candidates swapped."""
+    from oracle_rows import check_rows
+    g = load(case)
+    p = g["p"]
+    K = max(p["Ks"])
+    gold = g[f"cand_{K}"]
+    rows = np.nonzero(gold[:, 0] >= 0)[0][::7]
+    outs = tuple(g[f"m_{nm}_{K}"] for nm in ("idx", "s", "o", "sym", "err"))
+    got = check_rows(g["emb"], g["pool"], g["ranges"], gold, outs, rows, K, 8, chunk=16, label=case)
+    assert got["rows"] == len(rows)
+    bad = gold.copy()
+    tied = O.topk_rows(g["emb"], rows, K, 8)[3]
+    r = int(rows[np.nonzero(~tied)[0][len(rows) // 3]])  # a row whose top K + 1 scores are distinct
+    bad[r, [3, 4]] = bad[r, [4, 3]]
+    with pytest.raises(AssertionError):
+        check_rows(g["emb"], g["pool"], g["ranges"], bad, outs, [r], K, 8, label=case)
