@@ -70,6 +70,17 @@ def pmc_traffic(config: str):
     return d.get("sim_topk_hbm_bytes_per_launch"), f"profiles/pmc_{config}.json ({d.get('source', 'rocprofv3 PMC')})"
 
 
+def sq_summary(config: str):
+    """Executed-MFMA figures of the search's first pass from the committed SQ counter passes of THIS config
+    (profiles/sq_<config>.json, tools/sq_summary.py --json), else None."""
+    path = os.path.join(ROOT, "profiles", f"sq_{config}.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return d if d.get("config") == config else None
+
+
 def affine_hbm_roofline(dev, K: int, n_queries: int = 262_144, reps: int = 10) -> dict:
     """k_affine on a pool larger than the 256 MB Infinity Cache, so the candidate-row gathers are HBM traffic: the cfg4
     signal (60 min, 48 kHz: 86.4 M domains, a 2.76 GB pool), the real candidates of its first `n_queries` ranges
@@ -130,6 +141,28 @@ def affine_hbm_roofline(dev, K: int, n_queries: int = 262_144, reps: int = 10) -
             "equals_pipeline_output": same,
             "workload": f"cfg4 (60 min 48 kHz noise): the real top-{K} candidates of its first {q} ranges, pool of "
                         f"{nd} rows ({nd * rs * 4 / 1e9:.2f} GB, above the 256 MB MALL)"}
+
+
+def rank_share_roofline(sig, tile: int, K: int, nr: int, nd: int, world: int = 8, reps: int = 7) -> dict:
+    """The search of ONE rank's share at N = `world` (the last rank's contiguous block; cfg2 noise prunes nothing, so
+    the prune-balanced split of fwav.dist is the even one): its first pass + merge by HIP events on the launch
+    stream, as the algorithmic rate of the full-size line."""
+    from fwav import engine
+    lo = nr - nr // world
+    ms = []
+    for i in range(reps + 2):
+        ev = {}
+        r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=(lo, nr), events=ev, defer_ties=True)
+        r.wait()
+        torch.cuda.synchronize()
+        if i >= 2:
+            ms.append(ev["sim_topk"][0].elapsed_time(ev["sim_topk"][1]))
+    t = sorted(ms)[len(ms) // 2]
+    q = int(r.n_active.item())
+    tf = 2.0 * q * nd * 16 / (t * 1e-3) / 1e12
+    return {"world": world, "queries": q, "launch_ms": t, "achieved": tf, "unit": "TFLOP/s",
+            "frac": tf / F16_MFMA_PEAK_TF, "work": f"2*{q}*{nd}*16 flop (algorithmic, as `roofline`)",
+            "note": "median of the sim_topk stage over the reps; one rank's compute only (no broadcast / gather)"}
 
 
 def fwav_io_bench() -> dict:
@@ -302,11 +335,24 @@ def main():
         "roofline": {"kernel": f"{TOPK_KERNEL} (fp16 MFMA similarity GEMM pre-filter + streaming exact top-K)",
                      "bound": "mfma", "achieved": achieved_tf, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s",
                      "frac": achieved_tf / F16_MFMA_PEAK_TF, "traffic": traffic, "traffic_source": traffic_src,
-                     "work_per_launch": f"2*{n_active}*{nd}*16 = {flops:.4g} flop (one fp16 MFMA score per "
-                                        f"query-domain pair; exact f32 rescoring of survivors not counted)",
+                     "work_per_launch": f"2*{n_active}*{nd}*16 = {flops:.4g} flop: the ALGORITHMIC work of the "
+                                        f"reference's scores (every query-domain pair, fractal.py:537). The kernel "
+                                        f"does not execute it all: a centroid bound skips the (tile, query set) pairs "
+                                        f"that cannot reach a member's band, so `frac` is an effective rate; the "
+                                        f"MFMA work actually executed is `mfma_executed`",
                      "launch_ms": t_topk * 1e3, "rank": rank},
         "stage_ms": stage_ms,
     }
+    sq = sq_summary(args.config) if not sharded else None
+    if sq and sq.get("mfma_executed_flop_per_launch"):
+        ex_tf = sq["mfma_executed_flop_per_launch"] / t_topk / 1e12
+        line["roofline"]["mfma_executed"] = {
+            "flop_per_launch": sq["mfma_executed_flop_per_launch"], "achieved": ex_tf, "unit": "TFLOP/s",
+            "frac": ex_tf / F16_MFMA_PEAK_TF, "mfma_busy": sq.get("mfma_busy_frac"),
+            "wave_time": sq.get("wave_time"),
+            "note": "SQ_INSTS_MFMA x 32,768 flop (v_mfma_f32_32x32x16_f16) from the committed SQ pass of this config, "
+                    "over this run's launch time; mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles",
+            "source": f"profiles/sq_{args.config}.json ({sq.get('source')})"}
     if traffic:
         # the north star's "fraction of the HBM roofline" for the same launch: measured HBM bytes (PMC) over its time
         # (the kernel is bound by MFMA/VALU issue, not by HBM: its table is re-read from the Infinity Cache)
@@ -372,6 +418,7 @@ def main():
             line["fwav_io_cfg4"] = fwav_io_bench()
         except Exception as e:  # noqa: BLE001
             line["fwav_io_cfg4"] = {"error": str(e)[:200]}
+        line["roofline_rank_share"] = rank_share_roofline(sig, tile, K, nr, nd)
         line["roofline_affine"] = affine_hbm_roofline(dev, K)
         line["roofline_affine_in_pipeline"] = {
             "achieved": nr * (4 * rs + 4 * K + 4 * K * rs + 17) / (stage_ms["affine"] * 1e-3) / 1e9,

@@ -2,9 +2,11 @@
 tools/ab/sq_pmc.sh): per dispatch of k_sim_topk_f16's first pass, the shares of wave time (active / issue-stalled /
 parked), instruction counts per level-1 tile and per MFMA, and pipe utilisation per SIMD (SQ_* quad-cycle counters
 ×4; SQ_VALU_MFMA_BUSY_CYCLES in cycles; kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs).
-usage: python tools/sq_summary.py gpurun_out/sq [--tiles N]"""
+usage: python tools/sq_summary.py gpurun_out/sq [--tiles N] [--json profiles/sq_cfg2.json --config cfg2]
+(--json: the executed-MFMA figures bench.py puts beside its algorithmic roofline)"""
 import argparse
 import collections
+import json
 import csv
 import glob
 import os
@@ -33,6 +35,8 @@ def main():
     ap.add_argument("root")
     ap.add_argument("--tiles", type=float, default=646 * 8 * 41312,
                     help="level-1 tiles of one launch (cfg2: 646 blocks × 8 waves × 41,312 tiles)")
+    ap.add_argument("--json", default=None, help="write the executed-MFMA summary bench.py reads")
+    ap.add_argument("--config", default="cfg2")
     a = ap.parse_args()
     c = {}
     for v in load(a.root).values():
@@ -52,6 +56,20 @@ def main():
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_INSTS_BRANCH"):
         if k in c:
             print(f"{k:28s} {c[k]:.3e}  = {c[k] / t:5.2f} per level-1 tile")
+    if a.json:
+        # every MFMA of the search is v_mfma_f32_32x32x16_f16: 2·32·32·16 = 32,768 flop per wave instruction
+        d = {"config": a.config, "kernel": "k_sim_topk_f16 (first pass)",
+             "sq_insts_mfma_per_launch": c.get("SQ_INSTS_MFMA"),
+             "mfma_executed_flop_per_launch": c["SQ_INSTS_MFMA"] * 32768 if "SQ_INSTS_MFMA" in c else None,
+             "mfma_busy_frac": (c["SQ_VALU_MFMA_BUSY_CYCLES"] / SIMDS / cyc) if "SQ_VALU_MFMA_BUSY_CYCLES" in c
+             else None,
+             "kernel_cycles": cyc, "kernel_ms_at_2p4ghz": cyc / 2.4e6,
+             "wave_time": {"active": c["SQ_ACTIVE_INST_ANY"] / wc, "issue_stalled": c["SQ_WAIT_INST_ANY"] / wc,
+                           "parked": c["SQ_WAIT_ANY"] / wc},
+             "source": f"rocprofv3 --pmc SQ passes of tools/topk_once.py ({a.root})"}
+        with open(a.json, "w") as f:
+            json.dump(d, f, indent=1)
+        print(f"wrote {a.json}")
 
 
 if __name__ == "__main__":
