@@ -17,6 +17,11 @@
 #include "fwav_common.h"
 #include "../../include/fwav.h"
 
+// -DFWAV_AFF_* knobs build A/B variants of the debug library only (tools/ab_build.sh adds -DFWAV_DEBUG_API)
+#if !defined(FWAV_DEBUG_API) && (defined(FWAV_AFF_ABL) || defined(FWAV_AFF_BATCH) || defined(FWAV_AFF_XCD))
+#error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
+#endif
+
 namespace fwav {
 
 constexpr int kAffWaves = 4;

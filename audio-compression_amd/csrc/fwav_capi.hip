@@ -18,7 +18,7 @@ extern "C" {
 
 const char* fwav_last_error(void) { return fwav::g_err; }
 
-int fwav_abi_version(void) { return 4; }
+int fwav_abi_version(void) { return 5; }
 
 #ifndef FWAV_SOURCE_DIGEST
 #define FWAV_SOURCE_DIGEST "unknown"

@@ -23,8 +23,14 @@
 // HBM traffic is therefore ≈ (4·rs gathered + 13) B read + 4·rs B written per range per chunk, instead of
 // (12·rs + 17) B per range per iteration; the loop is bound by VALU issue.
 //
-// Δ is f64 here (BLAS sdot in the reference): only the early-exit decision can differ, and only when Δ lies
-// within rounding of eps.  The f64 sum has one canonical order — range → thread (sequential) → wave (xor tree)
+// Δ is f64 here; the reference's Δ is float32 from BLAS sdot norms (fractal.py:1460-1461, oracle.sdot_blas), and the
+// early exit takes the REFERENCE's decision: Δ_ref = Δ_exact·(1 + θ) with |θ| ≤ β = γ(L + 16) (L = ⌈n/64⌉ fma steps
+// of an sdot accumulator lane, the fold, the f32 sqrt and quotient; n = n_ranges·range_size), and Δ_f64 is within
+// 1e-7 of Δ_exact, so Δ_f64·(1 + β + 1e-7) < eps stops and Δ_f64·(1 − β − 1e-7) ≥ eps continues for certain.  An
+// iteration between the two (or whose sums reach f32's denormal / overflow range) stops the device loop "for a check"
+// (state[0] = 2) with recon before and after it in the two buffers; fwav_decode_exact then computes Δ_ref itself in
+// the sdot kernel's own order (k_decode_exact) and decides, and the host resumes the loop (fwav_decode_from) when it
+// goes on.  The f64 sum has one canonical order — range → thread (sequential) → wave (xor tree)
 // → block (kDecSpan ranges, fixed) → sum over blocks (fixed) — so a range-sharded decode (fwav.dist) whose shard
 // bounds are multiples of kDecSpan adds exactly the same partials and reproduces Δ bit-for-bit at any world size:
 // the ranks all-reduce the block partials (one non-zero contributor per entry, so the reduction is exact).
@@ -99,7 +105,9 @@ struct DecArgs {
   float* buf_a;
   float* buf_b;
   double* partials;   // [kDecIters][nblk_g][2]
-  int* state;         // done, iterations run, result buffer (0 = a, 1 = b), stop chunk
+  int* state;         // done (1 = stopped, 2 = stopped for the exact check), iterations run, result buffer (0 = a,
+                      // 1 = b), stop chunk
+  const float* init;  // the reconstruction before chunk 0 (nullptr: zeros, the reference's start)
   int64_t m;          // local ranges (this shard)
   int64_t blk0;       // global block index of local range 0 (shard lo / kDecSpan)
   int64_t nblk_g;     // blocks of the whole (unsharded) signal
@@ -126,15 +134,19 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_run(DecArgs a) {
     k = a.state[3];
     t0 = dec_t0(k, a.first);
     nit = a.state[1] - t0;
-    if (nit == dec_len(k, a.first, a.iterations)) return;  // stopped at the chunk's last iteration: already there
+    // stopped at the chunk's last iteration: already there (unless the exact check also needs the state before it)
+    if (nit == dec_len(k, a.first, a.iterations) && a.state[0] != 2) return;
   } else {
     if (a.state[0] != 0) return;
     k = a.chunk;
     t0 = dec_t0(k, a.first);
     nit = dec_len(k, a.first, a.iterations);
   }
-  const float* rin = k == 0 ? nullptr : dec_buf(a, k);
+  const float* rin = k == 0 ? a.init : dec_buf(a, k);
   float* rout = dec_buf(a, k + 1);
+  // FINISH for the exact check: the reconstruction before the stopping iteration goes to the chunk's other buffer
+  // (each thread's own ranges, after it read them: dec_buf(k) is the chunk's input for k ≥ 1, unused for k = 0)
+  float* rprev = (FINISH && a.state[0] == 2) ? dec_buf(a, k) : nullptr;
   const int rs = NFIX > 0 ? NFIX : a.rs;
   if constexpr (!FINISH) {
     for (int j = threadIdx.x; j < kDecIters * kDecWaves * 2; j += kDecThreads) (&acc[0][0][0])[j] = 0.0;
@@ -173,6 +185,17 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_run(DecArgs a) {
       for (int i = 0; i < RSMAX; ++i) rec[u][i] = (rin != nullptr && live && i < rs) ? rin[r * rs + i] : 0.0f;
     }
     for (int t = 0; t < nit; ++t) {
+      if (FINISH && rprev != nullptr && t == nit - 1) {
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          const int64_t r = r0 + u;
+          if (r < a.m) {
+#pragma unroll
+            for (int i = 0; i < RSMAX; ++i)
+              if (i < rs) rprev[r * rs + i] = rec[u][i];
+          }
+        }
+      }
       double rn = 0.0, dn = 0.0;
 #pragma unroll
       for (int u = 0; u < G; ++u) {
@@ -253,9 +276,23 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_sum(const double* __rest
   }
 }
 
-// Δ_t for the chunk's iterations in order; the first Δ_t < eps stops the loop.
+// The reference's decision for Δ_f64 = delta (sums rr = Σ rec², dd = Σ (next − rec)²): 1 stop, 0 go on, 2 not
+// certain (exact check).  Zero differences give Δ_ref = 0 exactly; sums in f32's denormal or overflow range are
+// always checked.
+__host__ __device__ inline int dec_decide(double rr, double dd, double delta, double eps, double beta) {
+  if (dd == 0.0) return 0.0 < eps ? 1 : 0;
+  if (dd < 1e-30 || dd > 1e36 || (rr > 0.0 && (rr < 1e-30 || rr > 1e36))) return 2;
+  const double b = beta + 1e-7;
+  if (delta * (1.0 + b) < eps) return 1;
+  if (delta * (1.0 - b) >= eps) return 0;
+  return 2;
+}
+// β for n = n_ranges·range_size values (see the header): ⌈n/64⌉ + 16 roundings of 2^-24, 1 % margin
+__host__ __device__ inline double dec_beta(int64_t n) { return 1.01 * (double)((n + 63) / 64 + 16) * 0x1p-24; }
+
+// Δ_t for the chunk's iterations in order; the first Δ_t < eps stops the loop (for certain, or for the exact check).
 __global__ void k_decode_stop(const double* __restrict__ sums, int chunk, int first, int iterations, double eps,
-                              int* __restrict__ state, double* __restrict__ deltas) {
+                              double beta, int* __restrict__ state, double* __restrict__ deltas) {
   if (threadIdx.x != 0 || state[0] != 0) return;
   const int t0 = dec_t0(chunk, first);
   const int nit = dec_len(chunk, first, iterations);
@@ -263,8 +300,9 @@ __global__ void k_decode_stop(const double* __restrict__ sums, int chunk, int fi
     const double nrm = sqrt(sums[2 * t]);
     const double delta = sqrt(sums[2 * t + 1]) / (nrm > 0.0 ? nrm : 1.0);
     deltas[t0 + t] = delta;
-    if (delta < eps) {
-      state[0] = 1;
+    const int dec = dec_decide(sums[2 * t], sums[2 * t + 1], delta, eps, beta);
+    if (dec != 0) {
+      state[0] = dec;
       state[1] = t0 + t + 1;
       state[2] = ((chunk + 1) & 1) ? 1 : 0;
       state[3] = chunk;
@@ -355,7 +393,7 @@ __global__ __launch_bounds__(kStreamThreads) void k_decode_iter(
   }
 }
 
-__global__ void k_decode_check(const double* __restrict__ partial, int nblocks, int it, double eps,
+__global__ void k_decode_check(const double* __restrict__ partial, int nblocks, int it, double eps, double beta,
                                int* __restrict__ state, double* __restrict__ deltas) {
   __shared__ double red[2][1024 / kWave];
   if (state[0]) return;
@@ -383,8 +421,108 @@ __global__ void k_decode_check(const double* __restrict__ partial, int nblocks, 
     const double delta = sqrt(dn) / (nrm > 0.0 ? nrm : 1.0);
     deltas[it] = delta;
     state[1] = it + 1;
-    state[2] = ((it + 1) & 1) ? 1 : 0;  // iteration it wrote recon_b when it is even
-    if (delta < eps) state[0] = 1;
+    state[2] = ((it + 1) & 1) ? 1 : 0;  // iteration it wrote recon_b when it is even (and read the other buffer)
+    state[0] = dec_decide(rn, dn, delta, eps, beta);
+  }
+}
+
+// ------------------------------------------------------------------ exact Δ (the early-exit check)
+// Δ_ref = f32(‖next − prev‖) / (‖prev‖ > 0 ? ‖prev‖ : 1) with both norms sqrt of the reference's BLAS sdot in its own
+// order (oracle.sdot_blas: 64 fma accumulator lanes over the first n & −64 values, fold, a 32-value step, horizontal
+// adds, then the tail in f64).  Every accumulator lane is one sequential fma chain, so one workgroup: waves 0 and 1
+// are the 64 lanes of ‖next − prev‖² and ‖prev‖² and consume 64-value blocks from LDS while all 16 waves stream the
+// next segment of both vectors into the other LDS half.
+constexpr int kExSeg = 64;  // blocks of 64 values per segment
+__device__ double exact_sdot_finish(const float* acc64, const float* __restrict__ x, const float* __restrict__ y,
+                                    int64_t n, bool diff) {
+  // fold of the 64 accumulators (lane 16k + j of group k), the optional 32-value step, the horizontal adds, the tail
+  const int64_t n1 = n & ~(int64_t)31, n64 = n1 & ~(int64_t)63;
+  auto val = [&](int64_t i) { return diff ? y[i] - x[i] : x[i]; };
+  double dot = 0.0;
+  if (n1 > 0) {
+    float a[4][8];
+    for (int k = 0; k < 4; ++k)
+      for (int j = 0; j < 8; ++j) a[k][j] = acc64[16 * k + j] + acc64[16 * k + j + 8];
+    if (n1 != n64)
+      for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 8; ++j) {
+          const float v = val(n64 + 8 * k + j);
+          a[k][j] = __builtin_fmaf(v, v, a[k][j]);
+        }
+    float v8[8];
+    for (int j = 0; j < 8; ++j) v8[j] = ((a[0][j] + a[1][j]) + a[2][j]) + a[3][j];
+    float h[4];
+    for (int j = 0; j < 4; ++j) h[j] = v8[j] + v8[j + 4];
+    dot = (double)((h[0] + h[1]) + (h[2] + h[3]));
+  }
+  for (int64_t i = n1; i < n; ++i) {
+    const float v = val(i);
+    dot += (double)(v * v);  // f32 product, f64 accumulation
+  }
+  return dot;
+}
+
+__global__ __launch_bounds__(1024) void k_decode_exact(const float* __restrict__ prev, const float* __restrict__ next,
+                                                       int64_t n, double eps, int t, double* __restrict__ deltas,
+                                                       int* __restrict__ state) {
+  __shared__ float lp[2][kExSeg * 64], ln[2][kExSeg * 64];
+  __shared__ float accs[2][64];
+  if (state[0] != 2) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int64_t n64 = (n & ~(int64_t)31) & ~(int64_t)63;
+  const int64_t nb = n64 / 64;
+  const int64_t nseg = cdiv(nb, kExSeg);
+  // thread tid stages floats [4·tid, 4·tid + 4) of each segment's 4,096 values of prev and next (one float4 each)
+  float4 rp, rn;
+  auto load = [&](int64_t sg) {
+    const int64_t i = sg * kExSeg * 64 + 4 * tid;
+    if (i + 4 <= n64) {
+      rp = *reinterpret_cast<const float4*>(prev + i);
+      rn = *reinterpret_cast<const float4*>(next + i);
+    } else {
+      float e[4], f[4];
+      for (int k = 0; k < 4; ++k) {
+        e[k] = i + k < n64 ? prev[i + k] : 0.0f;
+        f[k] = i + k < n64 ? next[i + k] : 0.0f;
+      }
+      rp = make_float4(e[0], e[1], e[2], e[3]);
+      rn = make_float4(f[0], f[1], f[2], f[3]);
+    }
+  };
+  auto store = [&](int buf) {
+    reinterpret_cast<float4*>(lp[buf])[tid] = rp;
+    reinterpret_cast<float4*>(ln[buf])[tid] = rn;
+  };
+  float acc = 0.0f;
+  if (nseg > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int64_t sg = 0; sg < nseg; ++sg) {
+    const int cur = (int)(sg & 1);
+    if (sg + 1 < nseg) load(sg + 1);
+    if (wave < 2) {
+      const int64_t bmax = nb - sg * kExSeg < kExSeg ? nb - sg * kExSeg : kExSeg;
+      for (int b = 0; b < bmax; ++b) {
+        const float x = lp[cur][b * 64 + lane];
+        const float v = wave == 0 ? ln[cur][b * 64 + lane] - x : x;  // recon_next − recon in f32 (fractal.py:1460)
+        acc = __builtin_fmaf(v, v, acc);
+      }
+    }
+    if (sg + 1 < nseg) store(cur ^ 1);  // the other half: last read in iteration sg − 1, before the barrier below
+    __syncthreads();
+  }
+  if (wave < 2) accs[wave][lane] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    const float sd = (float)exact_sdot_finish(accs[0], prev, next, n, true);
+    const float sr = (float)exact_sdot_finish(accs[1], prev, next, n, false);
+    const float nr = sqrtf(sr);
+    const float dl = sqrtf(sd) / (nr > 0.0f ? nr : 1.0f);
+    deltas[t] = (double)dl;
+    state[0] = (double)dl < eps ? 1 : 3;  // 3: the reference goes on — the caller resumes after iteration t
   }
 }
 
@@ -410,8 +548,10 @@ void launch_run(const DecArgs& a, int64_t nblk_local, hipStream_t st) {
 
 DecArgs make_args(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t m, int64_t lo,
                   int64_t nr_global, int rs, const float* pool, int iterations, int chunk, double eps,
-                  float s_clip, double s_damping, float* a, float* b, double* partials, int* state) {
+                  float s_clip, double s_damping, float* a, float* b, double* partials, int* state,
+                  const float* init) {
   DecArgs d;
+  d.init = init;
   d.idx = idx;
   d.s = s;
   d.o = o;
@@ -467,8 +607,8 @@ static int check_common(const void* idx, const void* s, const void* o, const voi
 // Sharded building blocks (the single-device fwav_decode below is exactly this sequence with lo = 0, m = nr).
 int fwav_decode_run(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t m,
                     int64_t lo, int64_t nr_global, int rs, const float* pool, int64_t nd, int iterations, int chunk,
-                    double eps, float s_clip, double s_damping, float* recon_a, float* recon_b, double* partials,
-                    int* state, void* stream) {
+                    double eps, float s_clip, double s_damping, const float* recon_init, float* recon_a,
+                    float* recon_b, double* partials, int* state, void* stream) {
   int rc = check_common(idx, s_in, o_in, sym, pool, recon_a, recon_b, state, m, rs, iterations, "fwav_decode_run");
   if (rc) return rc;
   FWAV_CHECK_ARG(partials, FWAV_ERR_ARG, "fwav_decode_run: null partials");
@@ -477,6 +617,8 @@ int fwav_decode_run(const int32_t* idx, const float* s_in, const float* o_in, co
                  FWAV_ERR_SHAPE, "fwav_decode_run: shard [%lld, %lld) of %lld not aligned to %d ranges",
                  (long long)lo, (long long)(lo + m), (long long)nr_global, kDecSpan);
   FWAV_CHECK_ARG(chunk >= 0 && chunk < fwav_decode_n_chunks(iterations, eps), FWAV_ERR_ARG, "fwav_decode_run: chunk");
+  FWAV_CHECK_ARG(recon_init != recon_a && recon_init != recon_b, FWAV_ERR_ARG,
+                 "fwav_decode_run: recon_init must not be one of the two loop buffers");
   (void)nd;
   hipStream_t st = (hipStream_t)stream;
   if (chunk == 0) (void)hipMemsetAsync(state, 0, 4 * sizeof(int), st);
@@ -484,32 +626,33 @@ int fwav_decode_run(const int32_t* idx, const float* s_in, const float* o_in, co
     (void)hipMemsetAsync(partials, 0, (size_t)kDecIters * dec_blocks(nr_global) * 2 * sizeof(double), st);
   if (m > 0) {
     DecArgs d = make_args(idx, s_in, o_in, sym, m, lo, nr_global, rs, pool, iterations, chunk, eps, s_clip,
-                          s_damping, recon_a, recon_b, partials, state);
+                          s_damping, recon_a, recon_b, partials, state, recon_init);
     launch_run<false>(d, dec_blocks(m), st);
   }
   FWAV_LAUNCH_CHECK("fwav_decode_run");
   return FWAV_OK;
 }
 
-int fwav_decode_reduce(const double* partials, int64_t nr_global, int iterations, int chunk, double eps,
-                       double* deltas, int* state, void* stream) {
+int fwav_decode_reduce(const double* partials, int64_t nr_global, int range_size, int iterations, int chunk,
+                       double eps, double* deltas, int* state, void* stream) {
   FWAV_CHECK_ARG(partials && deltas && state, FWAV_ERR_ARG, "fwav_decode_reduce: null pointer");
-  FWAV_CHECK_ARG(chunk >= 0 && chunk < fwav_decode_n_chunks(iterations, eps), FWAV_ERR_ARG,
+  FWAV_CHECK_ARG(chunk >= 0 && chunk < fwav_decode_n_chunks(iterations, eps) && range_size >= 1, FWAV_ERR_ARG,
                  "fwav_decode_reduce: chunk");
   const int first = dec_first(iterations, eps);
   hipStream_t st = (hipStream_t)stream;
   const int64_t nb = dec_blocks(nr_global);
   double* sums = (double*)partials + (int64_t)kDecIters * nb * 2;
   k_decode_sum<<<kDecIters, kDecThreads, 0, st>>>(partials, nb, sums, state, chunk, first, iterations);
-  k_decode_stop<<<1, kWave, 0, st>>>(sums, chunk, first, iterations, eps, state, deltas);
+  k_decode_stop<<<1, kWave, 0, st>>>(sums, chunk, first, iterations, eps, dec_beta(nr_global * range_size), state,
+                                     deltas);
   FWAV_LAUNCH_CHECK("fwav_decode_reduce");
   return FWAV_OK;
 }
 
 int fwav_decode_finish(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t m,
                        int64_t lo, int64_t nr_global, int rs, const float* pool, int64_t nd, int iterations,
-                       double eps, float s_clip, double s_damping, float* recon_a, float* recon_b, int* state,
-                       void* stream) {
+                       double eps, float s_clip, double s_damping, const float* recon_init, float* recon_a,
+                       float* recon_b, int* state, void* stream) {
   int rc = check_common(idx, s_in, o_in, sym, pool, recon_a, recon_b, state, m, rs, iterations, "fwav_decode_finish");
   if (rc) return rc;
   FWAV_CHECK_ARG(rs <= kMaxResidentRs, FWAV_ERR_SHAPE, "fwav_decode_finish: range_size %d > %d", rs, kMaxResidentRs);
@@ -517,29 +660,42 @@ int fwav_decode_finish(const int32_t* idx, const float* s_in, const float* o_in,
   hipStream_t st = (hipStream_t)stream;
   if (m > 0 && iterations > 0) {
     DecArgs d = make_args(idx, s_in, o_in, sym, m, lo, nr_global, rs, pool, iterations, 0, eps, s_clip, s_damping,
-                          recon_a, recon_b, nullptr, state);
+                          recon_a, recon_b, nullptr, state, recon_init);
     launch_run<true>(d, dec_blocks(m), st);
   }
   FWAV_LAUNCH_CHECK("fwav_decode_finish");
   return FWAV_OK;
 }
 
+int fwav_decode_exact(const float* prev, const float* next, int64_t n, double eps, int t, double* deltas, int* state,
+                      void* stream) {
+  FWAV_CHECK_ARG(prev && next && deltas && state && n >= 0 && t >= 0, FWAV_ERR_ARG, "fwav_decode_exact: bad args");
+  k_decode_exact<<<1, 1024, 0, (hipStream_t)stream>>>(prev, next, n, eps, t, deltas, state);
+  FWAV_LAUNCH_CHECK("fwav_decode_exact");
+  return FWAV_OK;
+}
+
 // Full decode loop on one device.  recon_a / recon_b: f32[nr*rs] buffers; after the call state[1] = iterations
 // run and state[2] selects the result (0 → recon_a, 1 → recon_b).  deltas: f64[iterations].  state: int[4].
-int fwav_decode(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t nr, int rs,
-                const float* pool, int64_t nd, int iterations, double eps, float s_clip, double s_damping,
-                float* recon_a, float* recon_b, double* deltas, int* state, void* workspace, size_t ws_bytes,
-                void* stream) {
+int fwav_decode_from(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t nr, int rs,
+                     const float* pool, int64_t nd, int iterations, double eps, float s_clip, double s_damping,
+                     const float* recon_init, float* recon_a, float* recon_b, double* deltas, int* state,
+                     void* workspace, size_t ws_bytes, void* stream) {
   int rc = check_common(idx, s_in, o_in, sym, pool, recon_a, recon_b, state, nr, rs, iterations, "fwav_decode");
   if (rc) return rc;
   FWAV_CHECK_ARG(ws_bytes >= fwav_decode_workspace_size(nr, rs, iterations) && workspace, FWAV_ERR_WORKSPACE,
                  "fwav_decode: workspace too small");
   FWAV_CHECK_ARG(iterations == 0 || deltas, FWAV_ERR_ARG, "fwav_decode: deltas required");
+  FWAV_CHECK_ARG(recon_init != recon_a && recon_init != recon_b, FWAV_ERR_ARG,
+                 "fwav_decode: recon_init must not be one of the two loop buffers");
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(state, 0, 4 * sizeof(int), st);
   if (nr == 0) return FWAV_OK;
-  if (iterations == 0) {  // the reference returns its zero-initialised buffer
-    (void)hipMemsetAsync(recon_a, 0, (size_t)nr * rs * sizeof(float), st);
+  if (iterations == 0) {  // the reference returns its zero-initialised buffer (or the state it resumed from)
+    if (recon_init != nullptr)
+      (void)hipMemcpyAsync(recon_a, recon_init, (size_t)nr * rs * sizeof(float), hipMemcpyDeviceToDevice, st);
+    else
+      (void)hipMemsetAsync(recon_a, 0, (size_t)nr * rs * sizeof(float), st);
     FWAV_LAUNCH_CHECK("fwav_decode");
     return FWAV_OK;
   }
@@ -548,38 +704,51 @@ int fwav_decode(const int32_t* idx, const float* s_in, const float* o_in, const 
     const int nchunks = fwav_decode_n_chunks(iterations, eps);
     for (int c = 0; c < nchunks; ++c) {
       rc = fwav_decode_run(idx, s_in, o_in, sym, nr, 0, nr, rs, pool, nd, iterations, c, eps, s_clip, s_damping,
-                           recon_a, recon_b, partials, state, stream);
+                           recon_init, recon_a, recon_b, partials, state, stream);
       if (rc) return rc;
-      rc = fwav_decode_reduce(partials, nr, iterations, c, eps, deltas, state, stream);
+      rc = fwav_decode_reduce(partials, nr, rs, iterations, c, eps, deltas, state, stream);
       if (rc) return rc;
     }
-    return fwav_decode_finish(idx, s_in, o_in, sym, nr, 0, nr, rs, pool, nd, iterations, eps, s_clip, s_damping,
-                              recon_a, recon_b, state, stream);
-  }
-  // range_size > 32: per-iteration streaming
-  (void)hipMemsetAsync(recon_a, 0, (size_t)nr * rs * sizeof(float), st);
-  char* w = (char*)workspace;
-  float* T = (float*)w;
-  float* md = T + nr * rs;
-  float* den = md + nr;
-  float* sst = den + nr;
-  float* ost = sst + nr;
-  double* partial = (double*)(((uintptr_t)(ost + nr) + 63) & ~(uintptr_t)63);
-  const int64_t nb = cdiv(nr, kStreamThreads);
-  const float c_keep = (float)(1.0 - s_damping);
-  const float c_opt = (float)s_damping;
-  const int use_d = s_damping > 0.0;
-  const float clipc = fabsf(s_clip);
-  k_decode_prepare<<<nb, kStreamThreads, 0, st>>>(idx, s_in, o_in, sym, nr, rs, pool, T, md, den, sst, ost);
-  for (int it = 0; it < iterations; ++it) {
-    const float* rec = (it & 1) ? recon_b : recon_a;
-    float* nx = (it & 1) ? recon_a : recon_b;
-    k_decode_iter<<<nb, kStreamThreads, 0, st>>>(T, md, den, sst, ost, nr, rs, clipc, c_keep, c_opt, use_d, rec, nx,
-                                                 partial, state);
-    k_decode_check<<<1, 1024, 0, st>>>(partial, (int)nb, it, eps, state, deltas);
+    rc = fwav_decode_finish(idx, s_in, o_in, sym, nr, 0, nr, rs, pool, nd, iterations, eps, s_clip, s_damping,
+                            recon_init, recon_a, recon_b, state, stream);
+    if (rc) return rc;
+  } else {
+    // range_size > 32: per-iteration streaming
+    if (recon_init != nullptr)
+      (void)hipMemcpyAsync(recon_a, recon_init, (size_t)nr * rs * sizeof(float), hipMemcpyDeviceToDevice, st);
+    else
+      (void)hipMemsetAsync(recon_a, 0, (size_t)nr * rs * sizeof(float), st);
+    char* w = (char*)workspace;
+    float* T = (float*)w;
+    float* md = T + nr * rs;
+    float* den = md + nr;
+    float* sst = den + nr;
+    float* ost = sst + nr;
+    double* partial = (double*)(((uintptr_t)(ost + nr) + 63) & ~(uintptr_t)63);
+    const int64_t nb = cdiv(nr, kStreamThreads);
+    const float c_keep = (float)(1.0 - s_damping);
+    const float c_opt = (float)s_damping;
+    const int use_d = s_damping > 0.0;
+    const float clipc = fabsf(s_clip);
+    k_decode_prepare<<<nb, kStreamThreads, 0, st>>>(idx, s_in, o_in, sym, nr, rs, pool, T, md, den, sst, ost);
+    for (int it = 0; it < iterations; ++it) {
+      const float* rec = (it & 1) ? recon_b : recon_a;
+      float* nx = (it & 1) ? recon_a : recon_b;
+      k_decode_iter<<<nb, kStreamThreads, 0, st>>>(T, md, den, sst, ost, nr, rs, clipc, c_keep, c_opt, use_d, rec, nx,
+                                                   partial, state);
+      k_decode_check<<<1, 1024, 0, st>>>(partial, (int)nb, it, eps, dec_beta(nr * rs), state, deltas);
+    }
   }
   FWAV_LAUNCH_CHECK("fwav_decode");
   return FWAV_OK;
+}
+
+int fwav_decode(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t nr, int rs,
+                const float* pool, int64_t nd, int iterations, double eps, float s_clip, double s_damping,
+                float* recon_a, float* recon_b, double* deltas, int* state, void* workspace, size_t ws_bytes,
+                void* stream) {
+  return fwav_decode_from(idx, s_in, o_in, sym, nr, rs, pool, nd, iterations, eps, s_clip, s_damping, nullptr, recon_a,
+                          recon_b, deltas, state, workspace, ws_bytes, stream);
 }
 
 }  // extern "C"

@@ -31,9 +31,28 @@
 // (score, index) keys that beat θ to the query's LDS buffer; a nearly full buffer is sorted (64-lane bitonic), cut
 // to its top K and θ set to the K-th score.  Domains stream in increasing index order, so a later domain whose
 // score equals θ can never displace an earlier one: strict '>' is exact.
+#include <algorithm>
 #include <type_traits>
 #include "fwav_common.h"
 #include "../../include/fwav.h"
+
+// Every compile-time knob below (-DFWAV_TOPK_*: geometry, tuning and experiment code paths) builds A/B variants of
+// the DEBUG library only (tools/ab_build.sh adds -DFWAV_DEBUG_API): a product build that sets one stops here, so
+// libfwav.so is always the measured default.
+#if !defined(FWAV_DEBUG_API) && (defined(FWAV_TOPK_ABL) || defined(FWAV_TOPK_APPOFF) || defined(FWAV_TOPK_CAP) || \
+    defined(FWAV_TOPK_CB) || defined(FWAV_TOPK_CENT) || defined(FWAV_TOPK_CENTSTATS) || \
+    defined(FWAV_TOPK_CENTWIDE) || defined(FWAV_TOPK_CENT_HL) || defined(FWAV_TOPK_CENT_L2OFF) || \
+    defined(FWAV_TOPK_CENT_MINQ) || defined(FWAV_TOPK_CG) || defined(FWAV_TOPK_CHAINS) || defined(FWAV_TOPK_CPDBL) || \
+    defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || defined(FWAV_TOPK_CVACC) || defined(FWAV_TOPK_CW) || \
+    defined(FWAV_TOPK_CWPE) || defined(FWAV_TOPK_DEBUG) || defined(FWAV_TOPK_DELTA) || defined(FWAV_TOPK_EXGROW) || \
+    defined(FWAV_TOPK_EXTSEED) || defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_G) || \
+    defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
+    defined(FWAV_TOPK_INTERLEAVE) || defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_MERGE_WG) || \
+    defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_QS) || defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || \
+    defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || \
+    defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE))
+#error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
+#endif
 
 namespace fwav {
 
@@ -426,13 +445,6 @@ __device__ __forceinline__ void stat_add_p(unsigned long long* stats, int i, uns
 }
 extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #define stat_add(i, v) stat_add_p(stats, (i), (v))
-// Experiment code paths exist only in the debug library (libfwav_debug.so, -DFWAV_DEBUG_API; tools/ab_build.sh):
-// the product library never carries them.
-#if !defined(FWAV_DEBUG_API) && (defined(FWAV_TOPK_EXTSEED) || defined(FWAV_TOPK_DEBUG) || \
-                                 defined(FWAV_TOPK_ABL) || defined(FWAV_TOPK_CENTSTATS) || \
-                                 defined(FWAV_TOPK_CENT_L2OFF) || defined(FWAV_TOPK_PADLDS))
-#error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
-#endif
 // Production geometry (the -D overrides build A/B variants: tools/ab_topk.py)
 #ifndef FWAV_TOPK_G
 #define FWAV_TOPK_G 4
@@ -468,26 +480,14 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifndef FWAV_TOPK_CB
 #define FWAV_TOPK_CB 2  // centroid level 2: (tile, set) pairs in flight together (4: +0.8 % cfg2, +10 % at 82,688 queries; 6, 8: spills)
 #endif
-#ifndef FWAV_TOPK_CRING
-#define FWAV_TOPK_CRING 0  // centroid geometry: a ring of this many slots of G chunks instead of the barrier (≥ 4)
-#endif
-#ifndef FWAV_TOPK_L2M32
-#define FWAV_TOPK_L2M32 0  // centroid level 2: 32-bit tile masks when a group has ≤ 32 tiles
-#endif
 #ifndef FWAV_TOPK_APPOFF
 #define FWAV_TOPK_APPOFF 1  // appends: running byte offset and a one-op key low word (else slot arithmetic per row)
-#endif
-#ifndef FWAV_TOPK_BSHARE
-#define FWAV_TOPK_BSHARE 0  // base geometry: read the pieces' shared limits every group too (else at window ends)
 #endif
 #ifndef FWAV_TOPK_CVACC
 #define FWAV_TOPK_CVACC 1  // centroid level 1: firing tiles accumulated per lane in a VGPR (else scalar masks per set)
 #endif
-#ifndef FWAV_TOPK_BRING
-#define FWAV_TOPK_BRING 0  // base geometry: the same ring (≥ 4)
-#endif
-#ifndef FWAV_TOPK_CDMA
-#define FWAV_TOPK_CDMA 0  // centroid geometry: the next group's DMA at the group top (0), after level 1 (1) / level 2 (2)
+#ifndef FWAV_TOPK_MERGE_WG
+#define FWAV_TOPK_MERGE_WG 12  // k_merge_pieces: persistent 4-wave workgroups per CU (2 / 6 / 12 / unbounded: cfg2 18.51 / 17.68 / 17.39 / 17.40 ms search)
 #endif
 #ifndef FWAV_TOPK_CSHARE
 #define FWAV_TOPK_CSHARE 1  // centroid geometry: read the pieces' shared limits every group (else at window ends)
@@ -518,13 +518,11 @@ constexpr int k16Sets = FWAV_TOPK_QS;   // query sets of 32 per wave (each LDS f
 #define FWAV_TOPK_CAP 256
 #endif
 constexpr int k16Cap = FWAV_TOPK_CAP;  // key-buffer entries per query (global workspace)
-#ifndef FWAV_TOPK_TRIG
-#define FWAV_TOPK_TRIG (FWAV_TOPK_CAP - 32)
-#endif
 #ifndef FWAV_TOPK_GROW
 #define FWAV_TOPK_GROW 64
 #endif
-constexpr int kTrig = FWAV_TOPK_TRIG;  // early compaction: buffer size ...
+// (A/B: triggers at 128 / 160 entries, cfg2 18.85 / 18.18 vs 17.50 ms, profiles/r04/ab_trig_*.log)
+constexpr int kTrig = k16Cap - 32;  // early compaction: buffer size ...
 constexpr int kGrow = FWAV_TOPK_GROW;  // ... and growth since the last compaction
 static_assert(k16Cap >= 128 && (k16Cap & (k16Cap - 1)) == 0, "the final bitonic sort needs a power-of-two buffer");
 // (A/B at cfg2: 512 entries 24.4 ms vs 21.2 ms for 256 — fewer compactions do not pay for the longer final sort)
@@ -1485,18 +1483,11 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   // 2 × G chunk slots: group g is consumed from one half while group g+1 streams into the other.
   // ALL of the kernel's LDS is one __shared__ object: beside a second one, hipcc waits vmcnt(0) for the in-flight
   // LDS DMA before the first ds_read of every chunk (cdna_hip_programming.md, "three .s-level traps" (a)).
-  // RING (experiment; narrow geometries, FWAV_TOPK_CRING / _BRING = NB ≥ 4 slots of G chunks): no workgroup
-  // barrier per group — each wave signals its chunk DMA landed (rdy) and the slot consumed (fin) on LDS counters, and
-  // waits only for what it needs: the group's chunks from every wave, and the slot it refills freed by every wave.
-  // Groups are prefetched PD = NB/2 ahead, so a wave may run up to PD groups ahead of the slowest one (a compaction
-  // or a window-end replay no longer stalls the other waves at once).
-  constexpr int NBR = CENT ? FWAV_TOPK_CRING : FWAV_TOPK_BRING;
-  constexpr bool RING = W <= 8 && NBR >= 4;
-  constexpr int NB = RING ? NBR : 2;
-  constexpr int PD = NB / 2;
+  // (Measured and rejected, tools/experiments/ring_and_knobs.patch: a ring of NB slots with LDS ready/free counters
+  // instead of the group barrier)
+  constexpr int NB = 2;
   struct Lds {
     u32x4 slots[NB * G][512];
-    uint32_t ring_rdy[NB], ring_fin[NB];
     Topk16SmemT<NG, STATS, !CENT, W> sm;
   };
   __shared__ __attribute__((aligned(16))) Lds lds_all;
@@ -1640,29 +1631,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   // retire the prologue's ordinary loads (query fragments, active list) before the stream, visibly to hipcc
   // (a load still pending at the loop head is waited on, vmcnt(0), inside every chunk iteration)
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  auto ring_ctr = [&](uint32_t* p) { return (__attribute__((address_space(3))) uint32_t*)(p); };
-  // spin (wave-uniform) until an LDS counter reaches target; bounded, so that a bug cannot hang the device
-  auto ring_wait = [&](uint32_t* p, uint32_t target) {
-    for (int it = 0; it < (1 << 21); ++it) {
-      const uint32_t v = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(ring_ctr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      if (v >= target) return;
-      __builtin_amdgcn_s_sleep(1);
-    }
-  };
-  auto ring_signal = [&](uint32_t* p) {
-    if (lane == 0) __hip_atomic_fetch_add(ring_ctr(p), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  if constexpr (RING) {
-    if (threadIdx.x < NB) {
-      lds_all.ring_rdy[threadIdx.x] = 0u;
-      lds_all.ring_fin[threadIdx.x] = 0u;
-    }
-    __syncthreads();  // (the waves without queries have exited: the barrier counts the remaining ones)
-    for (int gg = 0; gg < PD && gg < ngroups; ++gg) issue_group(gg);
-  } else if (ngroups > 0) {
-    issue_group(0);
-  }
+  if (ngroups > 0) issue_group(0);
 
   int sink = 0;     // ablation builds: keeps the MFMA / fold results of dbg 512/1024 alive
   int nfired[QS];  // wave-uniform FIFO tail: chunks recorded in sm.fired[group] so far
@@ -1681,22 +1650,6 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     const bool window_end =
         (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
     const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-    if constexpr (RING) {
-      if (g >= 1) {  // done with group g − 1's slot (its ds_reads retired)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        ring_signal(&lds_all.ring_fin[(g - 1) % NB]);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's chunk DMA of group g (and up to g + PD − 1)
-      if (STATS) stat_add(12, __builtin_amdgcn_s_memrealtime() - t_b0);
-      ring_signal(&lds_all.ring_rdy[g % NB]);
-      ring_wait(&lds_all.ring_rdy[g % NB], (uint32_t)(Wact * (g / NB + 1)));
-      if (g + PD < ngroups) {  // group g + PD into the slot of group g + PD − NB, once every wave has left it
-        if (g + PD - NB >= 0)
-          ring_wait(&lds_all.ring_fin[(g + PD - NB) % NB], (uint32_t)(Wact * ((g + PD - NB) / NB + 1)));
-        issue_group(g + PD);
-      }
-      asm volatile("" ::: "memory");
-    } else
     // RAW: own DMA of group g retired, then every wave's (barrier).  WAR: the other half was last read in
     // iteration g−1, whose ds_reads were all consumed before its waves reached this barrier.
     if (!(ABL && (dbg & 256))) {  // ablation 256: no group barrier (LDS races; timing only)
@@ -1707,11 +1660,10 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     }
     const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(7, t_b1 - t_b0);
-    // CENT, FWAV_TOPK_CDMA = 1 / 2: the next group's DMA issued after level 1 / after level 2 instead (a compaction's
-    // vmcnt(0) then need not wait for it)
-    if (!RING && g + 1 < ngroups && (!CENT || FWAV_TOPK_CDMA == 0)) issue_group(g + 1);
+    // (the DMA issued after level 1 or level 2 instead measured no better: profiles/r04/ab_prefix_dma_barrier.log)
+    if (g + 1 < ngroups) issue_group(g + 1);
     if (ABL && (dbg & 2)) continue;
-    if (((CENT && FWAV_TOPK_CSHARE) || (!CENT && FWAV_TOPK_BSHARE)) && share != nullptr) {
+    if (CENT && FWAV_TOPK_CSHARE && share != nullptr) {
       // CENT: the pieces' shared limits every group (a filter threshold that rises sooner skips more level-2 work)
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
@@ -1742,7 +1694,6 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           for (int s = 0; s < QS; ++s) pend[s] |= pc[s] << (8 * (c - cg));
         }
       }
-      if (!RING && FWAV_TOPK_CDMA == 1 && g + 1 < ngroups) issue_group(g + 1);
       if (STATS) {
         stat_add(13, __builtin_amdgcn_s_memrealtime() - t_l1);
         unsigned long long np = 0;
@@ -1756,8 +1707,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       // memory round trip per batch, as the base geometry's replays) and appended.
       static_for<QS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        // tile masks in 32 bits when a group has at most 32 tiles (half the scalar ops of the 64-bit bit walk)
-        using TMask = std::conditional_t<(FWAV_TOPK_L2M32 && 8 * G <= 32), uint32_t, uint64_t>;
+        using TMask = uint64_t;  // (32-bit masks for ≤ 32-tile groups: 17.15 vs 16.88 ms)
         TMask pm = (TMask)pend[s];
         TMask pass = 0;  // HL: tiles whose s16 passes the set's stream threshold
         while (pm != 0) {
@@ -1821,7 +1771,6 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           }
         }
       });
-      if (!RING && FWAV_TOPK_CDMA == 2 && g + 1 < ngroups) issue_group(g + 1);
     } else if (ABL && (dbg & (512 | 1024)) && c_end - cg == G) {
       // ablations 512: fold without ballots, 1024: MFMA without fold (outputs invalid)
       if (dbg & 1024)
@@ -1962,6 +1911,15 @@ __device__ __forceinline__ void merge_band(const uint64_t* __restrict__ sw, int 
   }
 }
 
+// One split-block query of k_merge_pieces (defined below the kernel).
+template <int C, int QB, bool HL>
+__device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int lane, uint64_t* sw,
+                                            const uint64_t* __restrict__ gkeys_all, const int32_t* __restrict__ active,
+                                            int n_active, int K, int32_t* __restrict__ cand,
+                                            int32_t* __restrict__ ovf_list, int32_t* __restrict__ n_ovf,
+                                            const uint32_t* __restrict__ share, const float* __restrict__ emb,
+                                            int64_t q_offset, const SgemvSplit& sp, int32_t* __restrict__ ties);
+
 template <int C, int QB, bool HL>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
@@ -1970,12 +1928,30 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
                                                       int32_t* __restrict__ n_ovf, const uint32_t* __restrict__ share,
                                                       const float* __restrict__ emb, int64_t q_offset, SgemvSplit sp,
                                                       int32_t* __restrict__ ties) {
-  constexpr int E = C / 64;
   const int n_active = *n_active_p;
   const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
-  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // split-block query index
-  if (plan.R == 0 || plan.halves || w >= plan.R * QB) return;
+  if (plan.R == 0 || plan.halves) return;
   const int lane = threadIdx.x & 63;
+  __shared__ uint64_t stage[4][C];
+  uint64_t* sw = stage[threadIdx.x >> 6];
+  // persistent waves (each looping over split-block queries; FWAV_TOPK_MERGE_WG workgroups per CU).  One workgroup
+  // per 4 queries measured the same (cfg2 search 17.40 vs 17.39 ms; 2 / 6 per CU: 18.51 / 17.68,
+  // profiles/r05/ab_merge_persistent.log): the merge (1.1 ms at cfg2, all 330,750 queries in 6 pieces) is bound by
+  // reading the pieces' bands, not by dispatch (profiles/r05/merge_sq_cfg2.log)
+  for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < plan.R * QB; w += (int64_t)gridDim.x * 4)
+    merge_query<C, QB, HL>(plan, w, lane, sw, gkeys_all, active, n_active, K, cand, ovf_list, n_ovf, share, emb,
+                           q_offset, sp, ties);
+}
+
+// One split-block query w of k_merge_pieces (whole wave; sw: the wave's LDS row).
+template <int C, int QB, bool HL>
+__device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int lane, uint64_t* sw,
+                                            const uint64_t* __restrict__ gkeys_all, const int32_t* __restrict__ active,
+                                            int n_active, int K, int32_t* __restrict__ cand,
+                                            int32_t* __restrict__ ovf_list, int32_t* __restrict__ n_ovf,
+                                            const uint32_t* __restrict__ share, const float* __restrict__ emb,
+                                            int64_t q_offset, const SgemvSplit& sp, int32_t* __restrict__ ties) {
+  constexpr int E = C / 64;
   const int64_t block = plan.F + w / QB;
   const int ql = (int)(w % QB);
   const int64_t qq = slot_query(block, ql, plan.nb, QB);
@@ -2031,8 +2007,6 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
     L = max(L, f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta));
   }
   // the band above L, compacted into the wave's LDS row, then into v (slot j·64 + lane)
-  __shared__ uint64_t stage[4][C];
-  uint64_t* sw = stage[threadIdx.x >> 6];
   int mb = 0;
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
@@ -2281,11 +2255,8 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(geo));
     if (pl.R > 0 && !pl.halves) (void)hipMemsetAsync(share, 0, (size_t)q1 * sizeof(uint32_t), st);
     const int mode1 = first_mode(nd);
-#ifndef FWAV_TOPK_PADLDS
-#define FWAV_TOPK_PADLDS 0  // experiment builds: dynamic LDS added to the base first pass (caps its occupancy)
-#endif
 #define FWAV_FIRST(MODE_, STATS_, DBG_, ST_)                                                                    \
-  k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, FWAV_TOPK_PADLDS, st>>>(                  \
+  k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, 0, st>>>(                  \
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, DBG_, ST_,  \
       sp, ties)
 #define FWAV_FIRST_WIDE(MODE_)                                                                                   \
@@ -2334,9 +2305,13 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
 #undef FWAV_FIRST_CENT
 #undef FWAV_FIRST_CENTW
     if (pl.R > 0) {
+      // persistent merge waves: ≈ 6 per SIMD (its occupancy), each looping over split-block queries
+      int cus, per_cu;
+      topk_device_slots(geo, cus, per_cu);
+      const int64_t mgrid_cap = (int64_t)cus * FWAV_TOPK_MERGE_WG;
 #define FWAV_MERGE(QB_, HL_)                                                                                    \
-  k_merge_pieces<k16Cap, QB_, HL_><<<cdiv(pl.R * QB_, 4), 256, 0, st>>>(gkeys, active, n_active, rt, P, K, cand, \
-                                                                       ovf1, n_ovf1, share, emb, q_offset, sp, ties)
+  k_merge_pieces<k16Cap, QB_, HL_><<<std::min<int64_t>(cdiv(pl.R * QB_, 4), mgrid_cap), 256, 0, st>>>(          \
+      gkeys, active, n_active, rt, P, K, cand, ovf1, n_ovf1, share, emb, q_offset, sp, ties)
       if (wide) {
         if (mode1 == kModeHL) FWAV_MERGE(kWideQB, true); else FWAV_MERGE(kWideQB, false);
       } else if (geo == kGeoCent) {

@@ -57,9 +57,11 @@ SIGNATURES = {
     "fwav_decode_chunk_iterations": (I32, []),
     "fwav_decode_n_chunks": (I32, [I32, F64]),
     "fwav_decode_partials_count": (SZ, [I64]),
-    "fwav_decode_run": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, I32, F64, F32, F64, P, P, P, P, P]),
-    "fwav_decode_reduce": (I32, [P, I64, I32, I32, F64, P, P, P]),
-    "fwav_decode_finish": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P]),
+    "fwav_decode_from": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, P, SZ, P]),
+    "fwav_decode_exact": (I32, [P, P, I64, F64, I32, P, P, P]),
+    "fwav_decode_run": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, I32, F64, F32, F64, P, P, P, P, P, P]),
+    "fwav_decode_reduce": (I32, [P, I64, I32, I32, I32, F64, P, P, P]),
+    "fwav_decode_finish": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P]),
 }
 
 #: the debug library's extra entry points (include/fwav_debug.h): the search's process-global test knobs and

@@ -15,7 +15,10 @@ Decompress (cfg5; fractal.py:1378-1473): rank 0 broadcasts the pool and scatters
 the iteration-resident decode kernel on its ranges; per chunk of up to 64 iterations the ranks all-reduce the
 per-block Δ partials (a few hundred KB) and take the same early-exit decision; the reconstruction is gathered to
 rank 0.  Shard bounds are multiples of ``fwav_decode_span()`` ranges, so Δ, the iteration count and the output
-are bit-identical to the single-GPU decode at any world size (fwav_decode.hip header).
+are bit-identical to the single-GPU decode at any world size (fwav_decode.hip header).  Where the f64 Δ cannot decide
+the reference's Δ < eps for certain, every rank stops for the check: the two reconstructions around that iteration
+are gathered to rank 0, which computes the reference's Δ in its own sdot order (fwav_decode_exact) and broadcasts
+the decision, and the ranks resume from their slices when the reference goes on.
 
 Collectives run on device tensors with RCCL and on host tensors with gloo (CPU tests, and the one-GPU rehearsal
 where ranks share cuda:0).  The per-rank compute is pluggable (``compute`` / ``decoder``) so the communication
@@ -279,6 +282,26 @@ def compress_sharded(signal: Optional[np.ndarray], tile_size: int, top_k: int, e
 
 
 # ---------------------------------------------------------------------------------------------- decompress
+def decode_beta(n: int) -> float:
+    """Relative bound between the reference's float32 Δ (BLAS sdot norms of n values) and the exact one
+    (fwav_decode.hip dec_beta)."""
+    return 1.01 * ((int(n) + 63) // 64 + 16) * 2.0 ** -24
+
+
+def decode_decision(rr: float, dd: float, delta: float, eps: float, beta: float) -> int:
+    """The device's early-exit decision for the f64 Δ (fwav_decode.hip dec_decide): 1 stop, 0 go on, 2 check."""
+    if dd == 0.0:
+        return 1 if 0.0 < eps else 0
+    if dd < 1e-30 or dd > 1e36 or (rr > 0.0 and (rr < 1e-30 or rr > 1e36)):
+        return 2
+    b = beta + 1e-7
+    if delta * (1.0 + b) < eps:
+        return 1
+    if delta * (1.0 - b) >= eps:
+        return 0
+    return 2
+
+
 def decode_span() -> int:
     from ._lib import size_call
     return size_call("fwav_decode_span")
@@ -303,9 +326,10 @@ class ShardDecoder:
     stream; the only host synchronisation is in :meth:`finish`."""
 
     def __init__(self, idx, s, o, sym, pool, lo, n_ranges_global, range_size, iterations, eps, s_clip=16.0,
-                 s_damping=0.0):
+                 s_damping=0.0, init: Optional[torch.Tensor] = None):
         from ._lib import size_call
         self.idx, self.s, self.o, self.sym, self.pool = idx, s, o, sym, pool
+        self.init = init  # the rank's reconstruction to start from (None: zeros) — a resumed loop
         self.dev = idx.device
         self.m, self.lo, self.nr, self.rs = int(idx.numel()), int(lo), int(n_ranges_global), int(range_size)
         self.nd = pool.numel() // self.rs
@@ -331,8 +355,11 @@ class ShardDecoder:
 
     def run(self, chunk: int) -> None:
         from ._lib import call
-        call("fwav_decode_run", *self._common(), chunk, self.eps, self.s_clip, self.s_damping, self.a.data_ptr(),
-             self.b.data_ptr(), self.partials.data_ptr(), self.state.data_ptr(), self._st())
+        call("fwav_decode_run", *self._common(), chunk, self.eps, self.s_clip, self.s_damping, self._init(),
+             self.a.data_ptr(), self.b.data_ptr(), self.partials.data_ptr(), self.state.data_ptr(), self._st())
+
+    def _init(self):
+        return None if self.init is None else self.init.data_ptr()
 
     def partials_prefix(self) -> torch.Tensor:
         """The block partials the ranks all-reduce (SUM) between run() and reduce()."""
@@ -340,20 +367,40 @@ class ShardDecoder:
 
     def reduce(self, chunk: int) -> None:
         from ._lib import call
-        call("fwav_decode_reduce", self.partials.data_ptr(), self.nr, self.iterations, chunk, self.eps,
+        call("fwav_decode_reduce", self.partials.data_ptr(), self.nr, self.rs, self.iterations, chunk, self.eps,
              self.deltas.data_ptr(), self.state.data_ptr(), self._st())
 
     def finish(self):
-        """→ (local reconstruction f32[m·rs] device tensor, iterations run, deltas list)."""
+        """→ (local reconstruction f32[m·rs] device tensor, iterations run, deltas list, pending): pending is None,
+        or — stopped for the exact check — the local reconstruction before the last iteration (the result is after
+        it)."""
         from ._lib import call
         if self.iterations == 0 or self.nr == 0:
-            return torch.zeros(self.m * self.rs, dtype=torch.float32, device=self.dev), 0, []
-        call("fwav_decode_finish", *self._common(), self.eps, self.s_clip, self.s_damping, self.a.data_ptr(),
-             self.b.data_ptr(), self.state.data_ptr(), self._st())
+            return torch.zeros(self.m * self.rs, dtype=torch.float32, device=self.dev), 0, [], None
+        call("fwav_decode_finish", *self._common(), self.eps, self.s_clip, self.s_damping, self._init(),
+             self.a.data_ptr(), self.b.data_ptr(), self.state.data_ptr(), self._st())
         st = self.state.cpu().numpy()
         ran = int(st[1])
-        out = self.b if int(st[2]) == 1 else self.a
-        return out[:self.m * self.rs], ran, self.deltas.cpu().numpy()[:ran].tolist()
+        out, other = (self.b, self.a) if int(st[2]) == 1 else (self.a, self.b)
+        pending = other[:self.m * self.rs] if int(st[0]) == 2 else None
+        return out[:self.m * self.rs], ran, self.deltas.cpu().numpy()[:ran].tolist(), pending
+
+    def exact_delta(self, prev: torch.Tensor, nxt: torch.Tensor) -> tuple[float, bool]:
+        """Rank 0: the reference's Δ between the whole signal's reconstructions (fwav_decode_exact) and whether it
+        stops the loop."""
+        from ._lib import call
+        st = torch.tensor([2, 0, 0, 0], dtype=torch.int32, device=self.dev)
+        d = torch.zeros(1, dtype=torch.float64, device=self.dev)
+        prev = prev.to(self.dev).contiguous()
+        nxt = nxt.to(self.dev).contiguous()
+        call("fwav_decode_exact", prev.data_ptr(), nxt.data_ptr(), prev.numel(), self.eps, 0, d.data_ptr(),
+             st.data_ptr(), self._st())
+        return float(d.item()), int(st[0].item()) == 1
+
+    def resumed(self, rec: torch.Tensor, iterations_left: int) -> "ShardDecoder":
+        """The same shard continuing from its reconstruction ``rec`` for ``iterations_left`` more iterations."""
+        return ShardDecoder(self.idx, self.s, self.o, self.sym, self.pool, self.lo, self.nr, self.rs, iterations_left,
+                            self.eps, self.s_clip, self.s_damping, init=rec.clone())
 
 
 def _all_reduce_sum_(t: torch.Tensor, group, device: torch.device) -> None:
@@ -366,14 +413,54 @@ def _all_reduce_sum_(t: torch.Tensor, group, device: torch.device) -> None:
     t.copy_(buf)
 
 
+def _gather_to_rank0(t: torch.Tensor, group, device: torch.device) -> Optional[torch.Tensor]:
+    """The ranks' local slices (in rank order = signal order) concatenated on rank 0; None elsewhere."""
+    cd = _coll_device(group, device)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=cd)
+    world = dist.get_world_size(group)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    buf = torch.zeros(max(max(ns), 1), dtype=t.dtype, device=cd)
+    buf[:t.numel()] = t.to(cd)
+    rank = dist.get_rank(group)
+    glist = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gather_list=glist, dst=0, group=group)
+    if rank != 0:
+        return None
+    return torch.cat([g[:k] for g, k in zip(glist, ns)])
+
+
 def decode_shard(decoder, group=None, device: Optional[torch.device] = None):
-    """Drive one rank's decoder through the chunk loop with the per-chunk all-reduce of Δ partials."""
+    """Drive one rank's decoder through the chunk loop with the per-chunk all-reduce of Δ partials.  A stop for the
+    exact early-exit check (fwav_decode.hip): both reconstructions gathered to rank 0, the reference's Δ there
+    (decoder.exact_delta), its decision broadcast, and the loop resumed on every rank when the reference goes on.
+    → (local reconstruction, iterations run, deltas)."""
     device = device or decoder.dev
-    for c in range(decoder.n_chunks):
-        decoder.run(c)
-        _all_reduce_sum_(decoder.partials_prefix(), group, device)
-        decoder.reduce(c)
-    return decoder.finish()
+    total = decoder.iterations
+    done, deltas = 0, []
+    while True:
+        for c in range(decoder.n_chunks):
+            decoder.run(c)
+            _all_reduce_sum_(decoder.partials_prefix(), group, device)
+            decoder.reduce(c)
+        rec, ran, dl, pending = decoder.finish()
+        done += ran
+        deltas += dl
+        if pending is None:
+            return rec, done, deltas
+        prev_all = _gather_to_rank0(pending, group, device)
+        next_all = _gather_to_rank0(rec, group, device)
+        cd = _coll_device(group, device)
+        verdict = torch.zeros(2, dtype=torch.float64, device=cd)
+        if dist.get_rank(group) == 0:
+            d_ref, stop = decoder.exact_delta(prev_all, next_all)
+            verdict[0], verdict[1] = d_ref, 1.0 if stop else 0.0
+        _broadcast_(verdict, group, device)
+        deltas[-1] = float(verdict[0].item())
+        if verdict[1].item() != 0.0 or done >= total:
+            return rec, done, deltas
+        decoder = decoder.resumed(rec, total - done)
 
 
 def decompress_sharded(matches_soa: Optional[dict], domains: Optional[np.ndarray], n_ranges: int, range_size: int,

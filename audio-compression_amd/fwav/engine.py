@@ -465,24 +465,38 @@ def _decompress_device(idx: torch.Tensor, s: torch.Tensor, o: torch.Tensor, sym:
                        n_ranges: int, range_size: int, iterations: int = 8, convergence_eps: float = 1e-3,
                        s_clip: float = 16.0, s_damping: float = 0.0):
     """decompress_audio's loop on device.  Returns (recon f32[n_ranges*range_size] tensor, iterations_run,
-    deltas f64 list).  One host synchronisation (to read the iteration count and the result buffer)."""
+    deltas f64 list).  One host synchronisation (to read the iteration count and the result buffer), plus one per
+    early-exit check: where the f64 Δ cannot decide the reference's Δ < eps (fractal.py:1460-1465), fwav_decode stops
+    for fwav_decode_exact (the reference's own sdot order) and the loop resumes when the reference goes on."""
     dev = idx.device
     st = _stream(dev)
     nr, rs = int(n_ranges), int(range_size)
     nd = pool.numel() // rs if rs > 0 else 0
     it = int(iterations)
+    eps = float(convergence_eps)
     a = torch.empty(max(nr * rs, 1), dtype=torch.float32, device=dev)
     b = torch.empty(max(nr * rs, 1), dtype=torch.float32, device=dev)
     deltas = torch.zeros(max(it, 1), dtype=torch.float64, device=dev)
     state = torch.zeros(4, dtype=torch.int32, device=dev)
     wsn = size_call("fwav_decode_workspace_size", nr, rs, it)
     ws = torch.empty(max(wsn, 16), dtype=torch.uint8, device=dev)
-    call("fwav_decode", idx.data_ptr(), s.data_ptr(), o.data_ptr(), sym.data_ptr(), nr, rs, pool.data_ptr(), nd, it,
-         float(convergence_eps), float(abs(F32(s_clip))), float(s_damping), a.data_ptr(), b.data_ptr(),
-         deltas.data_ptr(), state.data_ptr(), ws.data_ptr(), wsn, st)
-    stt = state.cpu().numpy()
-    ran = int(stt[1])
-    out = b if int(stt[2]) == 1 else a
+    done, init, out = 0, None, a
+    while True:
+        call("fwav_decode_from", idx.data_ptr(), s.data_ptr(), o.data_ptr(), sym.data_ptr(), nr, rs, pool.data_ptr(),
+             nd, it - done, eps, float(abs(F32(s_clip))), float(s_damping), _p(init), a.data_ptr(), b.data_ptr(),
+             deltas[done:].data_ptr(), state.data_ptr(), ws.data_ptr(), wsn, st)
+        stt = state.cpu().numpy()
+        ran = int(stt[1])
+        out, other = (b, a) if int(stt[2]) == 1 else (a, b)
+        if int(stt[0]) == 2:  # the reference's Δ decides: computed in its own sdot order
+            call("fwav_decode_exact", other.data_ptr(), out.data_ptr(), nr * rs, eps, ran - 1,
+                 deltas[done:].data_ptr(), state.data_ptr(), st)
+            if int(state[0].item()) == 3 and done + ran < it:  # it goes on: resume from this reconstruction
+                init = out.clone()
+                done += ran
+                continue
+        done += ran
+        break
     if nr == 0:
         out = a[:0]
-    return out[:nr * rs], ran, deltas.cpu().numpy()[:ran].tolist()
+    return out[:nr * rs], done, deltas.cpu().numpy()[:done].tolist()

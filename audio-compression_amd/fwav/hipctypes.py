@@ -241,13 +241,30 @@ def decompress(idx: np.ndarray, s: np.ndarray, o: np.ndarray, sym: np.ndarray, p
     d_state = DeviceBuffer.from_array(np.zeros(4, np.int32))
     wsn = size_call("fwav_decode_workspace_size", nr, rs, it)
     d_ws = DeviceBuffer(max(wsn, 16))
-    call("fwav_decode", *[b.value for b in d], nr, rs, d_pool.value, nd, it, float(convergence_eps),
-         float(abs(np.float32(s_clip))), float(s_damping), d_a.value, d_b.value, d_del.value, d_state.value,
-         d_ws.value, wsn, None)
-    call("fwav_stream_sync", None)
-    state = _i32(d_state, 4)
-    ran = int(state[1])
-    out = (d_b if int(state[2]) == 1 else d_a).to_array(np.float32, nr * rs)
+    eps = float(convergence_eps)
+    done, d_init = 0, None
+    while True:
+        call("fwav_decode_from", *[b.value for b in d], nr, rs, d_pool.value, nd, it - done, eps,
+             float(abs(np.float32(s_clip))), float(s_damping), None if d_init is None else d_init.value, d_a.value,
+             d_b.value, d_del.value + 8 * done, d_state.value, d_ws.value, wsn, None)
+        call("fwav_stream_sync", None)
+        state = _i32(d_state, 4)
+        ran = int(state[1])
+        res, other = (d_b, d_a) if int(state[2]) == 1 else (d_a, d_b)
+        if int(state[0]) == 2:  # the early-exit check in the reference's own sdot order (fractal.py:1460-1465)
+            call("fwav_decode_exact", other.value, res.value, nr * rs, eps, ran - 1, d_del.value + 8 * done,
+                 d_state.value, None)
+            call("fwav_stream_sync", None)
+            if int(_i32(d_state, 1)[0]) == 3 and done + ran < it:  # the reference goes on: resume from here
+                if d_init is None:
+                    d_init = DeviceBuffer(4 * max(nr * rs, 1))
+                _ck(hip().hipMemcpy(d_init.ptr, res.ptr, 4 * nr * rs, 3), "hipMemcpy")  # device to device
+                done += ran
+                continue
+        done += ran
+        break
+    ran = done
+    out = res.to_array(np.float32, nr * rs)
     if original_len is not None:
         out = out[:original_len]
     return out, ran, d_del.to_array(np.float64, max(it, 1))[:ran].tolist()

@@ -162,14 +162,34 @@ int fwav_debug_gather_rows(const float* table, int64_t n_rows, int rs, int64_t n
  * Replaces decompress_audio (fractal.py:1378-1473).  recon values are bit-exact with the reference.
  * fwav_decode runs the whole loop on one device with no host synchronisation: up to 64 iterations per launch
  * with each range's reconstruction held in registers (range_size <= 32), Δ = ‖next − rec‖/(‖rec‖ or 1) in f64 per
- * iteration from fixed-order partial sums, and a device flag that stops the loop at the first Δ < eps.
- * After the call: state[0] = stopped early, state[1] = iterations run t, state[2] = result buffer (0 → recon_a,
- * 1 → recon_b), deltas[0..t) = Δ per iteration.  state: int[4]; deltas: f64[iterations]. */
+ * iteration from fixed-order partial sums, and a device flag that stops the loop at the first iteration where the
+ * REFERENCE's Δ (float32 BLAS sdot norms, fractal.py:1460-1461) is < eps for certain — the f64 Δ and a proven bound
+ * on the two measures' difference decide — or, where the bound cannot decide, stops it "for a check".
+ * After the call: state[0] = 0 (every iteration ran), 1 (stopped: the reference stops here too) or 2 (stopped for the
+ * exact check), state[1] = iterations run t, state[2] = result buffer (0 → recon_a, 1 → recon_b), deltas[0..t) = Δ
+ * per iteration (f64 measure).  With state[0] = 2 the OTHER buffer holds the reconstruction before iteration t:
+ * fwav_decode_exact(prev = other buffer, next = result buffer, n_ranges·range_size, eps, t − 1, deltas, state)
+ * computes the reference's Δ in its own sdot order, stores it in deltas[t − 1] and sets state[0] = 1 (the reference
+ * stops) or 3 (it goes on: continue with fwav_decode_from, recon_init = a copy of the result buffer, the remaining
+ * iterations).  state: int[4]; deltas: f64[iterations]. */
 size_t fwav_decode_workspace_size(int64_t n_ranges, int range_size, int iterations);
 int fwav_decode(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t n_ranges,
                 int range_size, const float* pool, int64_t n_domains, int iterations, double eps, float s_clip,
                 double s_damping, float* recon_a, float* recon_b, double* deltas, int* state, void* workspace,
                 size_t ws_bytes, void* stream);
+/* fwav_decode starting from the reconstruction recon_init (device f32[n_ranges·range_size], not recon_a/recon_b;
+ * NULL = zeros, the reference's start) instead of zeros: the loop resumed after an exact check (iterations = the
+ * iterations left). */
+int fwav_decode_from(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t n_ranges,
+                     int range_size, const float* pool, int64_t n_domains, int iterations, double eps, float s_clip,
+                     double s_damping, const float* recon_init, float* recon_a, float* recon_b, double* deltas,
+                     int* state, void* workspace, size_t ws_bytes, void* stream);
+/* The early-exit check (only when state[0] == 2; a no-op otherwise): Δ_ref = f32(‖next − prev‖)/(‖prev‖ or 1), both
+ * norms sqrt of numpy's BLAS sdot in its own order (fractal.py:1460-1461) over n values — one workgroup, since each
+ * of the sdot's 64 accumulators is a sequential fma chain (≈ 10 ms at cfg5's 172.8 M values).  deltas[t] = Δ_ref;
+ * state[0] = 1 if Δ_ref < eps, else 3. */
+int fwav_decode_exact(const float* prev, const float* next, int64_t n, double eps, int t, double* deltas, int* state,
+                      void* stream);
 
 /* Range-sharded decode (multi-GPU, fwav.dist.decompress_sharded; range_size <= 32).  A rank owns ranges
  * [lo, lo + m) of n_ranges_global (idx/s/o/sym/recon are the rank's local slices; lo and, unless the shard ends the
@@ -177,23 +197,26 @@ int fwav_decode(const int32_t* idx, const float* s, const float* o, const uint8_
  * fwav_decode_chunk_iterations() iterations each; the first is 2 iterations when eps > 0):
  *   fwav_decode_run(c)  → the rank's block partials in partials[0 .. 2·chunk_iterations·ceil(n_ranges_global/span))
  *                         (other blocks zeroed); the caller all-reduces (SUM) that prefix across ranks;
- *   fwav_decode_reduce(c) → Δ per iteration and the stop decision, identical on every rank and bit-identical to the
- *                         single-device fwav_decode (one non-zero contributor per partial, fixed summation order);
- * then fwav_decode_finish() once.  partials holds fwav_decode_partials_count(n_ranges_global) doubles. */
+ *   fwav_decode_reduce(c) → Δ per iteration and the stop decision (as fwav_decode's), identical on every rank and
+ *                         bit-identical to the single-device fwav_decode (one non-zero contributor per partial, fixed
+ *                         summation order);
+ * then fwav_decode_finish() once.  partials holds fwav_decode_partials_count(n_ranges_global) doubles; recon_init
+ * (the rank's slice, or NULL = zeros) as fwav_decode_from.  After a stop for the check (state[0] == 2) the caller
+ * gathers the ranks' slices of both buffers and runs fwav_decode_exact on the whole signal's (fwav.dist). */
 int fwav_decode_span(void);
 int fwav_decode_chunk_iterations(void);
 int fwav_decode_n_chunks(int iterations, double eps);
 size_t fwav_decode_partials_count(int64_t n_ranges_global);
 int fwav_decode_run(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t m, int64_t lo,
                     int64_t n_ranges_global, int range_size, const float* pool, int64_t n_domains, int iterations,
-                    int chunk, double eps, float s_clip, double s_damping, float* recon_a, float* recon_b,
-                    double* partials, int* state, void* stream);
-int fwav_decode_reduce(const double* partials, int64_t n_ranges_global, int iterations, int chunk, double eps,
-                       double* deltas, int* state, void* stream);
+                    int chunk, double eps, float s_clip, double s_damping, const float* recon_init, float* recon_a,
+                    float* recon_b, double* partials, int* state, void* stream);
+int fwav_decode_reduce(const double* partials, int64_t n_ranges_global, int range_size, int iterations, int chunk,
+                       double eps, double* deltas, int* state, void* stream);
 int fwav_decode_finish(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t m, int64_t lo,
                        int64_t n_ranges_global, int range_size, const float* pool, int64_t n_domains, int iterations,
-                       double eps, float s_clip, double s_damping, float* recon_a, float* recon_b, int* state,
-                       void* stream);
+                       double eps, float s_clip, double s_damping, const float* recon_init, float* recon_a,
+                       float* recon_b, int* state, void* stream);
 
 #ifdef __cplusplus
 }

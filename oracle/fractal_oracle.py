@@ -517,11 +517,56 @@ def affine(ranges: np.ndarray, cand: np.ndarray, pool: np.ndarray, s_clip: float
 
 
 # ----------------------------------------------------------------------------------- decode (a7)
+def sdot_blas(x: np.ndarray, y: np.ndarray) -> np.float32:
+    """``x.dot(y)`` of two contiguous float32 vectors as numpy evaluates it (numpy → cblas_sdot, OpenBLAS 0.3.29
+    ``kernel/x86_64/sdot.c`` + ``sdot_microk_skylakex-2.c``; one thread whatever OpenBLAS's thread count — measured):
+    the first n1 = n & −32 entries by the vector kernel — 64 f32 fma accumulators (4 × 16 lanes; lane l of block b
+    takes entry 64b + l) over n & −64 entries, each folded to 8 lanes (a_k[j] = acc_k[j] + acc_k[j+8]), one more
+    32-entry fma step (4 × 8 lanes) when n1 is an odd multiple of 32, then ((a0 + a1) + a2) + a3, its upper and lower
+    four lanes added, two horizontal adds (h0 + h1) + (h2 + h3) — then the n − n1 tail products (rounded to f32) added
+    in f64, the sum rounded to f32.  Pinned against numpy: tests/test_oracle_golden.py::test_sdot_blas_pinned."""
+    x = np.ascontiguousarray(x, F32).reshape(-1)
+    y = np.ascontiguousarray(y, F32).reshape(-1)
+    n = len(x)
+    n1 = n & -32
+    n64 = n1 & -64
+    dot = 0.0
+    if n1:
+        xb = x[:n64].reshape(-1, 64).astype(np.float64)
+        yb = y[:n64].reshape(-1, 64).astype(np.float64)
+        acc = np.zeros(64, F32)
+        for b in range(len(xb)):  # one fma per lane per block, in block order
+            acc = fma_f32(xb[b] * yb[b], acc.astype(np.float64))
+        a = (acc.reshape(4, 16)[:, :8] + acc.reshape(4, 16)[:, 8:]).astype(F32)  # (4, 8)
+        if n1 != n64:
+            xt = x[n64:n1].reshape(4, 8).astype(np.float64)
+            yt = y[n64:n1].reshape(4, 8).astype(np.float64)
+            a = fma_f32(xt * yt, a.astype(np.float64))
+        v = ((a[0] + a[1]) + a[2]) + a[3]
+        h = v[:4] + v[4:]
+        dot = float((h[0] + h[1]) + (h[2] + h[3]))
+    for i in range(n1, n):
+        dot += float(x[i] * y[i])  # f32 product, f64 accumulation
+    return F32(dot)
+
+
+def reference_delta(recon: np.ndarray, nxt: np.ndarray) -> float:
+    """The convergence measure of decompress_audio (fractal.py:1460-1461) by the reference's own numpy calls:
+    ``norm(recon_next − recon) / (norm(recon) if norm(recon) > 0 else 1.0)`` on float32 arrays — np.linalg.norm of a
+    1-D float32 vector is sqrt(x.dot(x)) (BLAS sdot, sdot_blas), a float32; the quotient is float32, float() of it."""
+    r = np.ascontiguousarray(recon, F32).reshape(-1)
+    d = np.ascontiguousarray(nxt, F32).reshape(-1) - r
+    nr = np.linalg.norm(r)
+    denom = nr if nr > 0 else 1.0
+    return float(np.linalg.norm(d) / denom)
+
+
 def decode(idx, s_st, o_st, sym, pool, n_ranges, range_size, iterations=8, convergence_eps=1e-3,
-           original_len=None, s_clip=16.0, s_damping=0.0):
-    """decompress_audio (fractal.py:1378-1473), float32 in numpy order.  The convergence norm is computed
-    in float64 here (the reference uses BLAS sdot, fractal.py:1460-1461): only the early-exit decision
-    can differ, when Δ lies within rounding of eps.  Returns (recon f32, iterations_run, deltas)."""
+           original_len=None, s_clip=16.0, s_damping=0.0, deltas="f64"):
+    """decompress_audio (fractal.py:1378-1473), float32 in numpy order.  The early exit takes the reference's own
+    decision: Δ = reference_delta (numpy's BLAS sdot norms, fractal.py:1460-1461) < eps.  Returns (recon f32,
+    iterations_run, deltas): deltas="f64" lists Δ in float64 from exact float64 sums of the same float32 values (what the
+    device reports), deltas="reference" the reference's own float32-derived values."""
     idx = np.asarray(idx, np.int32).copy()
     s_st = np.asarray(s_st, F32).copy()
     o_st = np.asarray(o_st, F32).copy()
@@ -542,7 +587,7 @@ def decode(idx, s_st, o_st, sym, pool, n_ranges, range_size, iterations=8, conve
     valid = den > F32(1e-12)
     recon = np.zeros((nr, rs), F32)
     c = abs(F32(s_clip))
-    deltas = []
+    out_deltas = []
     it_run = 0
     for _ in range(iterations):
         mr = pw_mean(recon)
@@ -556,18 +601,21 @@ def decode(idx, s_st, o_st, sym, pool, n_ranges, range_size, iterations=8, conve
             s_used = np.where(valid, s_opt, s_st)
         s_used = np.clip(s_used, -c, c)
         nxt = F32(0.0) + (s_used[:, None] * tiles + o_st[:, None])   # bincount adds into +0.0
-        rn = float(np.sqrt(np.sum(recon.astype(np.float64) ** 2)))
-        dn = float(np.sqrt(np.sum((nxt - recon).astype(np.float64) ** 2)))  # f32 difference, as :1460
-        delta = dn / (rn if rn > 0 else 1.0)
+        delta = reference_delta(recon, nxt)
+        if deltas == "f64":
+            rn = float(np.sqrt(np.sum(recon.astype(np.float64) ** 2)))
+            dn = float(np.sqrt(np.sum((nxt - recon).astype(np.float64) ** 2)))  # f32 difference, as :1460
+            out_deltas.append(dn / (rn if rn > 0 else 1.0))
+        else:
+            out_deltas.append(delta)
         recon = nxt
-        deltas.append(delta)
         it_run += 1
         if delta < convergence_eps:
             break
     out = recon.reshape(-1)
     if original_len is not None:
         out = out[:original_len]
-    return out, it_run, deltas
+    return out, it_run, out_deltas
 
 
 # ----------------------------------------------------------------------------------- .fwav (format)

@@ -67,8 +67,21 @@ def test_debug_library_split(lib):
     assert lib.lib() is lib.product_lib()
 
 
+def test_every_knob_is_guarded():
+    """Every compile-time knob of the kernels (#ifndef / #ifdef FWAV_TOPK_* / FWAV_AFF_*) is named in its file's
+    product-build guard (#error without -DFWAV_DEBUG_API), so no -D override can reach libfwav.so."""
+    import re
+    for f, pre in (("fwav_topk.hip", "FWAV_TOPK_"), ("fwav_affine.hip", "FWAV_AFF_")):
+        src = open(os.path.join(ROOT, "audio-compression_amd", "csrc", f)).read()
+        knobs = set(re.findall(r"#ifn?def (" + pre + r"\w+)", src))
+        guard = src[src.index("#if !defined(FWAV_DEBUG_API) && ("):]
+        guard = guard[:guard.index("#error")]
+        named = set(re.findall(r"defined\((" + pre + r"\w+)\)", guard))
+        assert knobs and knobs <= named, (f, sorted(knobs - named))
+
+
 @pytest.mark.parametrize("switch", ["FWAV_TOPK_ABL=1", "FWAV_TOPK_EXTSEED", "FWAV_TOPK_DEBUG", "FWAV_TOPK_CENTSTATS",
-                                    "FWAV_TOPK_CENT_L2OFF", "FWAV_TOPK_PADLDS=0"])
+                                    "FWAV_TOPK_CENT_L2OFF", "FWAV_TOPK_G=2", "FWAV_TOPK_CB=4"])
 def test_product_build_refuses_experiment_switches(switch):
     """An experiment code path compiled without -DFWAV_DEBUG_API stops the build (#error): the product library can
     carry none of them (libfwav_debug.so, built with -DFWAV_DEBUG_API, is where they compile)."""
@@ -84,7 +97,7 @@ def test_product_build_refuses_experiment_switches(switch):
 
 def test_error_codes_without_gpu(lib):
     L = lib.lib()
-    assert L.fwav_abi_version() == 4
+    assert L.fwav_abi_version() == 5
     rc = L.fwav_affine(None, 10, 8, None, 64, None, 100, 16.0, None, None, None, None, None, None)
     assert rc == -1 and b"null" in L.fwav_last_error()
     rc = L.fwav_sim_topk(None, None, 10, None, None, 10, 0, 64, 1, None, None, None, 0, None)

@@ -194,8 +194,9 @@ class CpuChunkDecoder:
 
     CI = 64
 
-    def __init__(self, idx, s, o, sym, pool, lo, nr, rs, iterations, eps, s_clip=16.0, s_damping=0.0):
+    def __init__(self, idx, s, o, sym, pool, lo, nr, rs, iterations, eps, s_clip=16.0, s_damping=0.0, init=None):
         from oracle import fractal_oracle as O
+        self.args = (idx, s, o, sym, pool, lo, nr, rs)
         self.O = O
         F32 = np.float32
         idx = idx.numpy().copy()
@@ -223,9 +224,9 @@ class CpuChunkDecoder:
                                                    1 + -(-(iterations - self.first) // self.CI))
         self.nblk = -(-max(nr, 1) // SPAN)
         self.part = torch.zeros(self.CI * self.nblk * 2, dtype=torch.float64)
-        self.rec = np.zeros((self.m, rs), F32)
+        self.rec = np.zeros((self.m, rs), F32) if init is None else init.numpy().reshape(self.m, rs).copy()
         self.start = self.rec
-        self.deltas, self.ran, self.stopped = [], 0, False
+        self.deltas, self.ran, self.stopped, self.prev = [], 0, False, None
 
     def _t0(self, c):
         return 0 if c == 0 else self.first + (c - 1) * self.CI
@@ -265,22 +266,33 @@ class CpuChunkDecoder:
     def reduce(self, chunk):
         if self.stopped:
             return
+        from fwav.dist import decode_beta, decode_decision
         p = self.part.view(self.CI, self.nblk, 2).numpy()
         for t in range(self._len(chunk)):
             rn, dn = float(np.sum(p[t, :, 0])), float(np.sum(p[t, :, 1]))
             d = np.sqrt(dn) / (np.sqrt(rn) if rn > 0 else 1.0)
             self.deltas.append(d)
             self.ran = self._t0(chunk) + t + 1
-            if d < self.eps:
+            dec = decode_decision(rn, dn, d, self.eps, decode_beta(self.nr * self.rs))
+            if dec != 0:
                 self.stopped = True
                 rec = self.start
-                for _ in range(t + 1):
+                for _ in range(t):
                     rec = self._step(rec)
-                self.rec = rec
+                self.prev = rec if dec == 2 else None
+                self.rec = self._step(rec)
                 return
 
     def finish(self):
-        return torch.from_numpy(self.rec.reshape(-1).copy()), self.ran, self.deltas
+        pend = None if self.prev is None else torch.from_numpy(self.prev.reshape(-1).copy())
+        return torch.from_numpy(self.rec.reshape(-1).copy()), self.ran, self.deltas, pend
+
+    def exact_delta(self, prev, nxt):
+        d = self.O.reference_delta(prev.numpy(), nxt.numpy())
+        return d, d < self.eps
+
+    def resumed(self, rec, left):
+        return CpuChunkDecoder(*self.args, left, self.eps, float(self.c), self.damp, init=rec)
 
 
 def _dec_worker(rank, world, port, soa, pool, nr, rs, kw, q):
@@ -340,14 +352,8 @@ def test_sharded_decompress_equals_oracle(world):
         ref, it, rdel = O.decode(soa["idx"], soa["s"], soa["o"], soa["sym"], pool, nr, rs, **kw)
         assert info["iterations"] == it
         assert np.array_equal(rec.view(np.uint32), ref.view(np.uint32))
-        np.testing.assert_allclose(info["deltas"], rdel, rtol=1e-12)
-        one = CpuChunkDecoder(*(torch.from_numpy(soa[f]) for f in ("idx", "s", "o", "sym")), torch.from_numpy(pool),
-                              0, nr, rs, kw.get("iterations", 8), kw.get("convergence_eps", 1e-3),
-                              s_damping=kw.get("s_damping", 0.0))
-        for c in range(one.n_chunks):
-            one.run(c)
-            one.reduce(c)
-        assert one.finish()[2] == info["deltas"]
+        # f64 Δ, except at an iteration the exact check decided (the reference's float32 value there)
+        np.testing.assert_allclose(info["deltas"], rdel, rtol=1e-6)
 
 
 def test_decode_bounds_aligned():
@@ -359,3 +365,33 @@ def test_decode_bounds_aligned():
         assert all(a % 4096 == 0 for a, _ in b)
         sizes = [c - a for a, c in b]
         assert max(sizes) - min(sizes) <= 4096 or nr < 4096 * world
+
+
+@pytest.mark.parametrize("side", ["stop", "go_on"])
+def test_sharded_decompress_exact_check(side):
+    """The early exit where the f64 Δ cannot decide (fractal.py:1460-1465): eps placed inside the certified band of an
+    iteration whose reference Δ (float32 BLAS sdot norms) and f64 Δ differ — just above the reference's Δ (it stops
+    there) or just below it (it goes on: every rank resumes from its slice).  Two gloo ranks take the reference's
+    decision (the oracle's iteration count and reconstruction, bit for bit)."""
+    from fwav.dist import decode_beta
+    from oracle import fractal_oracle as O
+    rng = np.random.default_rng(11)
+    nr, nd, rs = 3000, 700, 8
+    pool = rng.normal(0, 0.3, (nd, rs)).astype(np.float32)
+    soa = dict(idx=rng.integers(0, nd, nr).astype(np.int32), s=rng.uniform(-1, 1, nr).astype(np.float32),
+               o=rng.normal(0, 0.1, nr).astype(np.float32), sym=(rng.random(nr) < 0.5).astype(np.uint8))
+    base = dict(iterations=40, s_damping=0.5)
+    args = (soa["idx"], soa["s"], soa["o"], soa["sym"], pool, nr, rs)
+    _, _, d64 = O.decode(*args, convergence_eps=0.0, **base)
+    _, _, dref = O.decode(*args, convergence_eps=0.0, deltas="reference", **base)
+    beta = decode_beta(nr * rs)
+    t = next(t for t in range(5, 40) if dref[t] != d64[t])
+    eps = dref[t] * (1 + beta / 4) if side == "stop" else dref[t] * (1 - beta / 4)
+    assert abs(eps - d64[t]) < beta * d64[t]  # inside the band: the device cannot decide on its own
+    kw = dict(base, convergence_eps=eps)
+    ref, it, _ = O.decode(*args, **kw)
+    assert (it == t + 1) == (side == "stop")
+    rec, info = _run_world(_dec_worker, 2, (soa, pool, nr, rs, kw))
+    assert info["iterations"] == it
+    assert np.array_equal(rec.view(np.uint32), ref.view(np.uint32))
+    assert info["deltas"][t] == dref[t]  # the checked iteration reports the reference's own Δ

@@ -76,6 +76,33 @@ def test_decode_bitexact(case):
         d, it, dl = O.decode(*args, iterations=12, convergence_eps=0.0, s_damping=0.3, original_len=p["original_len"])
         assert bit_equal(d, g[f"decd_{K}"])
         np.testing.assert_allclose(dl, g[f"decd_deltas_{K}"], rtol=1e-5)
+        # the reference's own Δ values (BLAS sdot norms) as its log prints them ({delta:.6e}, the goldens' source),
+        # every one of them
+        _, _, dr = O.decode(*args, iterations=12, convergence_eps=0.0, s_damping=0.3, deltas="reference")
+        assert [float(f"{v:.6e}") for v in dr] == [float(v) for v in g[f"decd_deltas_{K}"]]
+        _, _, dr = O.decode(*args, deltas="reference")
+        assert [float(f"{v:.6e}") for v in dr] == [float(v) for v in g[f"dec_deltas_{K}"]]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_decode_early_exit_takes_reference_decision(case):
+    """The stop decision is the reference's (Δ from numpy's BLAS sdot norms, fractal.py:1460-1465), not the float64
+    measure's: with eps placed strictly between the two at an iteration where they differ, the oracle stops exactly
+    where the reference's Δ says."""
+    g = load(case)
+    p = g["p"]
+    K = max(p["Ks"])
+    args = (g[f"m_idx_{K}"], g[f"m_s_{K}"], g[f"m_o_{K}"], g[f"m_sym_{K}"], g["pool"], len(g[f"m_idx_{K}"]), p["rs"])
+    _, _, d64 = O.decode(*args, iterations=12, convergence_eps=0.0, s_damping=0.3)
+    _, _, ref = O.decode(*args, iterations=12, convergence_eps=0.0, s_damping=0.3, deltas="reference")
+    cand = [t for t in range(len(ref)) if ref[t] != d64[t] and all(ref[u] >= max(ref[t], d64[t]) for u in range(t))]
+    if not cand:
+        pytest.skip("no iteration where the two measures differ (and none before it is as small)")
+    t = cand[0]
+    lo, hi = sorted((ref[t], d64[t]))
+    eps = (lo + hi) / 2
+    _, it, _ = O.decode(*args, iterations=12, convergence_eps=eps, s_damping=0.3)
+    assert it == (t + 1 if ref[t] < eps else min(12, next((u + 1 for u in range(t + 1, 12) if ref[u] < eps), 12)))
 
 
 @pytest.mark.parametrize("case", [c for c in CASES if c in ("tone", "sweep", "ragged", "tiny")])
@@ -179,3 +206,19 @@ def test_full_size_row_checker_accepts_reference_rows(case):
     bad[r, [3, 4]] = bad[r, [4, 3]]
     with pytest.raises(AssertionError):
         check_rows(g["emb"], g["pool"], g["ranges"], bad, outs, [r], K, 8, label=case)
+
+
+@pytest.mark.parametrize("n", [0, 1, 31, 32, 33, 63, 64, 65, 95, 96, 97, 127, 128, 129, 1000, 4097, 65537, 200003])
+def test_sdot_blas_pinned(n):
+    """O.sdot_blas (the order of np.linalg.norm's BLAS sdot, fractal.py:1460-1461) equals numpy's own x.dot(y) bit for
+    bit, at 1 and 8 OpenBLAS threads (the single-threaded result is numpy's at any thread count)."""
+    from threadpoolctl import threadpool_limits
+    rng = np.random.default_rng(n)
+    for trial in range(2):
+        x = (rng.standard_normal(n) * np.exp(rng.uniform(-4, 4, n))).astype(np.float32)
+        y = rng.standard_normal(n).astype(np.float32)
+        for T in (1, 8):
+            with threadpool_limits(T, user_api="blas"):
+                for a, b in ((x, x), (x, y)):
+                    want = a.dot(b) if n else np.float32(0)
+                    assert O.sdot_blas(a, b).view(np.uint32) == np.float32(want).view(np.uint32), (n, T)

@@ -1,5 +1,5 @@
 """Run the cfg2 similarity search once (after one warm-up) with a given dbg value — a target for rocprofv3 --pmc.
-usage: python tools/topk_once.py [dbg]"""
+usage: [AB_NQ=n] [AB_GEO=g] [AB_LIB=lib] python tools/topk_once.py [dbg]"""
 import os as _os_dbg
 _os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
@@ -34,12 +34,15 @@ ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
      emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
-active = torch.arange(nr, dtype=torch.int32, device="cuda")
-n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
+nq = int(os.environ.get("AB_NQ", nr))  # active queries (the first nq ranges; default all)
+if os.environ.get("AB_GEO"):  # first-pass geometry override (0 base, 1 wide, 2 centroid, 3 centroid wide)
+    call("fwav_debug_topk_geometry", int(os.environ["AB_GEO"]))
+active = torch.arange(nq, dtype=torch.int32, device="cuda")
+n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
 cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
-wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nr, nd, 64), dtype=torch.uint8, device="cuda")
+wsk = torch.empty(size_call("fwav_sim_topk_workspace_size", nq, nd, 64), dtype=torch.uint8, device="cuda")
 for _ in range(2):
-    call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nr, 0,
+    call("fwav_debug_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
          64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), dbg, None, st)
 torch.cuda.synchronize()
 print("done", dbg)
