@@ -669,7 +669,8 @@ int fwav_decode_finish(const int32_t* idx, const float* s_in, const float* o_in,
 
 int fwav_decode_exact(const float* prev, const float* next, int64_t n, double eps, int t, double* deltas, int* state,
                       void* stream) {
-  FWAV_CHECK_ARG(prev && next && deltas && state && n >= 0 && t >= 0, FWAV_ERR_ARG, "fwav_decode_exact: bad args");
+  FWAV_CHECK_ARG(((prev && next) || n == 0) && deltas && state && n >= 0 && t >= 0, FWAV_ERR_ARG,
+                 "fwav_decode_exact: bad args");
   k_decode_exact<<<1, 1024, 0, (hipStream_t)stream>>>(prev, next, n, eps, t, deltas, state);
   FWAV_LAUNCH_CHECK("fwav_decode_exact");
   return FWAV_OK;

@@ -9,6 +9,7 @@ pipeline of compress_audio (fractal.py:1040-1256, :556-632, :757-870) and decomp
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 
@@ -17,16 +18,33 @@ from . import _lib
 from ._lib import FwavError, call, size_call
 from .nporder import blas_threads, numpy_topk_row, zero_query_candidates
 
-_lib.TORCH_FREE = True  # this host never imports torch: libfwav.so binds the system HIP runtime
+# this host never imports torch: unless torch is already there, libfwav.so binds the system HIP runtime (and hip()
+# then reuses whichever runtime it bound)
+_lib.TORCH_FREE = "torch" not in sys.modules
 
 _HIP = None
 H2D, D2H = 1, 2
 
 
+def _mapped_runtime():
+    """Path of the HIP runtime already mapped into this process (/proc/self/maps), if any."""
+    try:
+        with open("/proc/self/maps") as f:
+            paths = sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln and "/" in ln})
+    except OSError:
+        return None
+    return paths[0] if paths else None
+
+
 def hip():
+    """The HIP runtime libfwav.so is bound to: libfwav.so is loaded first (it binds torch's runtime when torch came
+    first, else the system one), and that very library — found in /proc/self/maps — serves the buffers here, so a
+    process never maps a second runtime through this module."""
     global _HIP
     if _HIP is None:
-        for p in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+        _lib.product_lib()
+        mapped = _mapped_runtime()
+        for p in ([mapped] if mapped else []) + ["libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"]:
             try:
                 _HIP = C.CDLL(p)
                 break

@@ -128,9 +128,11 @@ def _slot(i: int, numel: int) -> torch.Tensor:
 
 
 def score_row_launches(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, threads: int,
-                       stream: int, budget: int = DEVICE_ROW_BUDGET):
-    """Yield (first row, device f32[m·nd] scores, event) per fwav_score_rows launch of at most ``budget`` bytes,
-    each launch queued on the current stream (``stream``) when the generator reaches it."""
+                       stream: int, budget: int = DEVICE_ROW_BUDGET, first_row: int = 0):
+    """Yield (first row + first_row, device f32[m·nd] scores, event) per fwav_score_rows launch of at most
+    ``budget`` bytes, each launch queued on the current stream (``stream``) when the generator reaches it.  A
+    consumer that must hold one launch at a time delegates with ``yield from`` (a loop variable of its own would keep
+    the previous launch alive while this generator allocates the next)."""
     nd = int(n_domains)
     n = rows.numel()
     per = max(1, min(n, budget // (4 * nd)))
@@ -142,7 +144,7 @@ def score_row_launches(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int,
              stream)
         ev = torch.cuda.Event()
         ev.record()
-        yield b0, S, ev
+        yield b0 + first_row, S, ev
         del S, ev  # not held while the next launch allocates: one launch's rows on the device at a time
 
 
@@ -196,31 +198,60 @@ def rank_rows(launches, n: int, n_domains: int, k: int, copy_stream=None) -> lis
     return futs
 
 
+#: device bytes of score rows launched eagerly (on the caller's stream, right after a slice's tie check) by all the
+#: rank_rows_async calls still in flight together; a call past it launches every batch on the driver's side
+PIPE_EAGER_TOTAL = 32 << 30
+_EAGER_LOCK = threading.Lock()
+_EAGER_BYTES = 0
+_ROWS: dict = {}
+
+
 def rank_rows_async(rows: torch.Tensor, *, emb: torch.Tensor, n_domains: int, q_offset: int, k: int, threads: int,
                     stream: int, budget: int = PIPE_ROW_BUDGET):
     """Queue the exact score rows of ``rows`` now — at most ``budget`` bytes of them, in one launch — and copy + rank
     them on the driver thread (copies on a copy stream that waits for the launches).  Returns a Future of the n row
     futures.  Used between the query sub-blocks of one search (fwav.engine), so that the next sub-block's search does
     not delay the score rows: only their copies and numpy's ranking overlap it.  Rows beyond the budget (a periodic
-    input can tie thousands of rows, 345 MB each at cfg4) are launched lazily by the driver thread, one budget at a
-    time as the earlier ones reach the host, so the device holds at most ``budget`` bytes of score rows per slice."""
+    input can tie thousands of rows, 345 MB each at cfg4) are launched by the driver thread, one budget at a time as
+    the earlier ones reach the host, on a side stream that waits only for this call's point in the caller's stream
+    (not for what the caller queues after it: the next slice's search).  The eager first launch is skipped when the
+    calls in flight already hold PIPE_EAGER_TOTAL of eager rows, so at most max(budget, PIPE_EAGER_TOTAL) + budget
+    bytes of score rows are on the device however many slices are pending."""
+    global _EAGER_BYTES
     n = rows.numel()
     dev = rows.device
-    cur = torch.cuda.current_stream(dev)  # the launches' stream (``stream``): their events are recorded on it
-    gen = score_row_launches(rows, emb=emb, n_domains=n_domains, q_offset=q_offset, threads=threads, stream=stream,
-                             budget=budget)
-    first = [next(gen)] if n else []
+    cur = torch.cuda.current_stream(dev)  # the caller's stream (``stream``): the eager launch goes here
+    ready = torch.cuda.Event()
+    ready.record(cur)  # everything this call's rows depend on (the slice's search and tie check)
     key = str(dev)
     if key not in _COPY:
         _COPY[key] = torch.cuda.Stream(dev)
-    cs = _COPY[key]
+        _ROWS[key] = torch.cuda.Stream(dev)
+    cs, side = _COPY[key], _ROWS[key]
+    nd = int(n_domains)
+    per = max(1, min(n, budget // (4 * nd))) if n else 0
+    nbytes = 4 * nd * per
+    with _EAGER_LOCK:
+        eager = n > 0 and _EAGER_BYTES + nbytes <= max(PIPE_EAGER_TOTAL, nbytes)
+        if eager:
+            _EAGER_BYTES += nbytes
+    first = [next(score_row_launches(rows[:per], emb=emb, n_domains=nd, q_offset=q_offset, threads=threads,
+                                     stream=stream, budget=budget))] if eager else []
+    rest = rows[per:] if eager else rows
 
     def job():
         def it():  # each launch's scores are released once its rows are on the host
-            while first:
+            global _EAGER_BYTES
+            if first:
                 yield first.pop(0)
-            with torch.cuda.stream(cur):
-                yield from gen
+                with _EAGER_LOCK:
+                    _EAGER_BYTES -= nbytes
+            if rest.numel():
+                with torch.cuda.stream(side):
+                    side.wait_event(ready)
+                    yield from score_row_launches(rest, emb=emb, n_domains=nd, q_offset=q_offset, threads=threads,
+                                                  stream=side.cuda_stream, budget=budget,
+                                                  first_row=per if eager else 0)
         with torch.cuda.device(dev):
             return rank_rows(it(), n, n_domains, k, copy_stream=cs)
 

@@ -136,10 +136,13 @@ def test_debug_search_rejects_workspace_of_another_query_count(lib):
     sizes = {q: L.fwav_sim_topk_workspace_size(q, nd, 64) for q in (20672, 41344, 65536, 82688, 131072)}
     # a workspace sized for more queries can be too small for fewer (their plan splits more blocks into pieces)
     # (the sizes also cover the centroid geometry's plans, which can make them monotonic in the query count)
-    pairs = [(a, b) for a in sizes for b in sizes if b < a and sizes[b] > sizes[a]]
+    pairs = [(b, sizes[a]) for a in sizes for b in sizes if b < a and sizes[b] > sizes[a]]
     p = ctypes.c_void_p(16)
-    cases = [(pairs[0][1], sizes[pairs[0][0]])] if pairs else []
-    for q, ws in cases + [(20672, sizes[20672] - 1), (41344, sizes[20672])]:
+    # always: one byte short of every query count's own size, and every smaller size of another count (a larger
+    # count's workspace handed to a smaller count whose plan needs more, whenever the sizes are not monotonic)
+    cases = [(q, sizes[q] - 1) for q in sizes] + [(q, ws) for q in sizes for ws in sizes.values() if ws < sizes[q]]
+    assert len(cases) >= 2 * len(sizes) and all(c in cases for c in pairs)
+    for q, ws in cases:
         rc = L.fwav_debug_sim_topk(p, p, nd, p, p, q, 0, 64, p, p, ws, 0, None, None)
         assert rc == -5 and b"workspace" in L.fwav_last_error(), (q, ws)
 
@@ -211,7 +214,8 @@ def test_work_plan_covers_every_query(lib, n, rt, pieces, wide):
     with lib.debug_library():
         lib.call("fwav_debug_topk_plan_cover", n, rt, pieces, wide, count.ctypes.data, ctypes.addressof(items))
     qb = lib.debug_lib().fwav_debug_topk_qb(wide)  # queries per block of the geometry
-    assert qb == 32 * (16 if wide in (1, 3) else 8) * (1 if wide < 2 else qb // (512 if wide == 3 else 256))
+    # base 8 waves × 32, wide 16 × 32, centroid 8 waves × 2 sets × 32, centroid-wide 16 × 2 × 32
+    assert qb == {0: 256, 1: 512, 2: 512, 3: 1024}[wide]
     nb = -(-n // qb)
     P = 1 if pieces == 1 else (2 if pieces == -1 else pieces)
     R = 0 if P == 1 else min(nb, rt)
@@ -236,7 +240,8 @@ print("HIP", "torch" in sys.modules, hip)
 """
 
 
-@pytest.mark.parametrize("pre", ["", "from fwav import hipctypes"])
+@pytest.mark.parametrize("pre", ["", "from fwav import hipctypes\nhipctypes.hip()",
+                                 "import torch\nfrom fwav import hipctypes\nhipctypes.hip()"])
 def test_one_hip_runtime_per_process(lib, pre):
     """libfwav.so loaded with no torch imported yet must still leave ONE HIP runtime in the process: PyTorch-ROCm
     ships its own libamdhip64, and a library that bound the system one first left torch a second runtime that saw no
@@ -250,9 +255,9 @@ def test_one_hip_runtime_per_process(lib, pre):
     torch_loaded = line[0].split()[1] == "True"
     hip = eval(line[0].split(" ", 2)[2])
     assert len(hip) == 1, hip
-    if pre:
+    if pre and "import torch" not in pre:
         assert not torch_loaded and "/torch/" not in hip[0]
-    else:
+    else:  # torch first (or the product host importing it): its runtime, reused by hipctypes.hip()
         try:
             import torch  # noqa: F401
             assert torch_loaded and "/torch/" in hip[0]

@@ -144,7 +144,8 @@ def test_exact_delta_kernel_equals_reference(n):
         st = td(np.array([2, 0, 0, 0], np.int32))
         d = td(np.zeros(1))
         from fwav._lib import call
-        call("fwav_decode_exact", td(p_).data_ptr(), td(q_).data_ptr(), n, 1.0, 0, d.data_ptr(), st.data_ptr(),
+        dp, dq = td(p_), td(q_)  # held: a temporary's memory would be handed to the next allocation
+        call("fwav_decode_exact", dp.data_ptr(), dq.data_ptr(), n, 1.0, 0, d.data_ptr(), st.data_ptr(),
              torch.cuda.current_stream().cuda_stream)
         want = O.reference_delta(p_, q_)
         assert float(d.item()) == want, (n, float(d.item()), want)

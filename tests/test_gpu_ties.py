@@ -81,3 +81,31 @@ def test_rank_rows_async_device_memory_is_bounded(cfg2_table):
         r = int(rows[j])
         ref = O.numpy_topk_row(O.sgemv_scores(emb, emb[r][None, :], kinds)[0], K)
         assert np.array_equal(got[j], ref), r
+
+
+def test_rank_rows_async_many_slices_bounded(cfg2_table, monkeypatch):
+    """Several slices' rankings in flight at once (the sliced search queues one per slice before any finishes): the
+    eager launches stop at PIPE_EAGER_TOTAL (here 2 budgets), the rest go through the driver's side stream one budget
+    at a time, so the device peak stays ≈ PIPE_EAGER_TOTAL + one budget — and every row is still numpy's ranking."""
+    res = cfg2_table
+    nd = res.n_domains
+    T = ties.blas_threads()
+    budget = 4 * 4 * nd
+    monkeypatch.setattr(ties, "PIPE_EAGER_TOTAL", 2 * budget)
+    slices = [torch.arange(s0, s0 + 40, dtype=torch.int32, device=dev()) for s0 in range(0, 240, 40)]
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    futs = [ties.rank_rows_async(r, emb=res.emb, n_domains=nd, q_offset=0, k=K, threads=T,
+                                 stream=torch.cuda.current_stream().cuda_stream, budget=budget) for r in slices]
+    got = [np.stack([f.result() for f in fu.result()]) for fu in futs]
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    print(f"6 slices x 40 rows through {budget / 1e6:.1f} MB budgets: peak {peak / 1e6:.1f} MB")
+    assert peak <= 3 * budget + (4 << 20)
+    assert ties._EAGER_BYTES == 0
+    emb = res.emb.view(-1, 16).cpu().numpy()
+    kinds = O.sgemv_col_kind(np.arange(nd), nd, T)
+    for j, r in ((0, 0), (3, 17), (5, 39)):
+        q = int(slices[j][r])
+        assert np.array_equal(got[j][r], O.numpy_topk_row(O.sgemv_scores(emb, emb[q][None, :], kinds)[0], K)), q
