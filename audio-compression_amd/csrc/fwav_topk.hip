@@ -48,9 +48,9 @@
     defined(FWAV_TOPK_EXTSEED) || defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_G) || \
     defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
     defined(FWAV_TOPK_INTERLEAVE) || defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_MERGE_WG) || \
-    defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_QS) || defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || \
-    defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || \
-    defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE))
+    defined(FWAV_TOPK_MSKIP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
+    defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || \
+    defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE))
 #error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
 #endif
 
@@ -485,6 +485,17 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #endif
 #ifndef FWAV_TOPK_CVACC
 #define FWAV_TOPK_CVACC 1  // centroid level 1: firing tiles accumulated per lane in a VGPR (else scalar masks per set)
+#endif
+#ifndef FWAV_TOPK_PRIO
+// wave priorities (bits): 1 waves W/2.. at prio 1, 2 compactions at prio 2, 4 centroid level 2 + appends at prio 1
+// (the part of a group whose length varies from wave to wave: the group barrier waits for it), 8 the base geometry's
+// window-end replays at prio 1.  Same-box A/B, identical outputs (profiles/r05/ab_prio.log): cfg2 17.46 → 17.24 /
+// 17.27 ms with 4 (2: 17.33 / 17.38, 6: 17.39 / 17.44, 1: +0.5 %, 3: +2.5 %), 165,375 queries 9.77 → 9.61; adding 8:
+// cfg3 179.8 → 178.3 ms, one rank's eighth and quarter within ±0.5 %
+#define FWAV_TOPK_PRIO 12
+#endif
+#ifndef FWAV_TOPK_MSKIP
+#define FWAV_TOPK_MSKIP 1  // k_merge_pieces: the radix select starts below the key bits the union shares
 #endif
 #ifndef FWAV_TOPK_MERGE_WG
 #define FWAV_TOPK_MERGE_WG 12  // k_merge_pieces: persistent 4-wave workgroups per CU (2 / 6 / 12 / unbounded: cfg2 18.51 / 17.68 / 17.39 / 17.40 ms search)
@@ -1053,6 +1064,7 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
   // limit sooner, once the buffer passes kTrig and has grown by kGrow since its last compaction
   uint64_t need = __ballot(lane < 32 && (total > C - 32 || (total > kTrig && total >= kept + kGrow) ||
                                          (EX && FWAV_TOPK_EXGROW > 0 && total >= kept + FWAV_TOPK_EXGROW)));
+  if ((FWAV_TOPK_PRIO & 2) && need != 0ull) __builtin_amdgcn_s_setprio(2);  // the barrier's critical path
   while (need != 0ull) {
     const int l = __builtin_ctzll(need);
     need &= need - 1;
@@ -1075,6 +1087,10 @@ __device__ __forceinline__ float append_tile(const floatx16& acc, float thf, int
       if (!EX && sm.ovf[qg * 32 + l]) thf = INFINITY;
       if (EX) *kthp = kth_l;
     }
+  }
+  if (FWAV_TOPK_PRIO & 2) {  // back to the wave's base priority
+    if ((FWAV_TOPK_PRIO & 1) && (threadIdx.x >> 6) >= (blockDim.x >> 7)) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
   }
   return thf;
 }
@@ -1600,6 +1616,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     }, bc, cslack);
   }
   const int nchunks = (int)cdiv(nd, kChunk);  // < 2^31 / 256: chunk arithmetic stays 32-bit (scalar)
+  if ((FWAV_TOPK_PRIO & 1) && wave >= W / 2) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half
   // this item's chunk range [c0, c1) (the whole table unless the block is split)
   const int c0 = (int)((int64_t)nchunks * piece / npieces), c1 = (int)((int64_t)nchunks * (piece + 1) / npieces);
   const int ngroups = (c1 - c0 + G - 1) / G;
@@ -1655,6 +1672,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     if (!(ABL && (dbg & 256))) {  // ablation 256: no group barrier (LDS races; timing only)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       if (STATS) stat_add(12, __builtin_amdgcn_s_memrealtime() - t_b0);
+      if (FWAV_TOPK_PRIO & 4) __builtin_amdgcn_s_setprio(0);
       if (!(ABL && (dbg & 16384))) __builtin_amdgcn_s_barrier();  // 16384: own DMA wait, no barrier
       asm volatile("" ::: "memory");
     }
@@ -1701,6 +1719,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
         for (int s = 0; s < QS; ++s) np += __popcll(pend[s]);
         stat_add(14, np);
       }
+      if (FWAV_TOPK_PRIO & 4) __builtin_amdgcn_s_setprio(1);
       // level 2: the marked (tile, set) pairs scored with the set's queries, kCentBatch at a time (their fragments and
       // MFMAs in flight together).  S16: survivors appended at once.  HL: the pairs whose s16 can pass are collected
       // first, then refined in batches of kReplayBatch with their low-part fragments fetched from L2 together (one
@@ -1795,6 +1814,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       }
       // each wave replays its own fired chunks (compacting inline when a buffer fills); compile-time set indices
       // (static_for): a runtime-indexed per-set array would live in scratch / LDS
+      if (!CENT && (FWAV_TOPK_PRIO & 8)) __builtin_amdgcn_s_setprio(1);
       static_for<QS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
         if constexpr (!CENT) {
@@ -1804,6 +1824,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
                                              stats, sp, emb, qv[s], &kth[s], share);
         }
       });
+      if (!CENT && (FWAV_TOPK_PRIO & 8)) __builtin_amdgcn_s_setprio(0);
       if (STATS) stat_add(4, __builtin_amdgcn_s_memrealtime() - t_c);
       // retire the replay's loads and stores here, visibly to hipcc's wait bookkeeping (vmcnt(0) expcnt(7)
       // lgkmcnt(15)): otherwise it keeps them "pending" at the loop head and waits on them before the next
@@ -1996,7 +2017,27 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
   uint32_t L = Lk;
   if (seed == 0u && m > K) {
     uint32_t T = 0;
-    for (int bit = 31; bit >= (HL ? 0 : 12); --bit) {
+    int top = 31;
+    if (FWAV_TOPK_MSKIP) {
+      // the bits every key of the union shares decide nothing: start the select below them (the greedy select takes
+      // each shared 1 bit and leaves each shared 0 bit, so T = the shared prefix there)
+      uint32_t a = ~0u, o = 0u;
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (u < nu && x[u] != 0ull) {
+          a &= (uint32_t)(x[u] >> 32);
+          o |= (uint32_t)(x[u] >> 32);
+        }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        a &= (uint32_t)__shfl_xor((int)a, off);
+        o |= (uint32_t)__shfl_xor((int)o, off);
+      }
+      const uint32_t d = a ^ o;
+      top = d == 0u ? -1 : 31 - __builtin_clz(d);
+      T = (top < 0 ? a : a & ~((2u << top) - 1u)) & ~((1u << (HL ? 0 : 12)) - 1u);  // the select's resolution
+    }
+    for (int bit = top; bit >= (HL ? 0 : 12); --bit) {
       const uint32_t Tc = T | (1u << bit);
       int c = 0;
 #pragma unroll
