@@ -49,8 +49,9 @@
     defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
     defined(FWAV_TOPK_INTERLEAVE) || defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_MERGE_WG) || \
     defined(FWAV_TOPK_MSKIP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
-    defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || \
-    defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE))
+    defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SETSTATS) || \
+    defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || \
+    defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE))
 #error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
 #endif
 
@@ -1344,6 +1345,11 @@ constexpr int kCentBatch = FWAV_TOPK_CB;
 #ifdef FWAV_TOPK_CENTSTATS
 __device__ unsigned long long g_cent_stats[4];  // experiment builds: level-1 tiles, level-2 (tile, set) pairs
 #endif
+#ifdef FWAV_TOPK_SETSTATS
+// experiment builds: per (item, query set) the ticks of its level 2 + appends, per (item, wave) the ticks waited at
+// the group barrier and the wave's whole time (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_set_ticks[1 << 16], g_wave_wait[1 << 16], g_wave_total[1 << 16];
+#endif
 template <int QS>
 __device__ __forceinline__ uint64_t cent_set_mask(int s) {
   static_assert(QS == 2 || QS == 4 || QS == 8, "centroid sets: 2, 4 or 8 query sets per wave");
@@ -1606,15 +1612,25 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     for (int s = 0; s < QS; ++s)
       if (upd[s]) thf[s] = fmaxf(thf[s], inseed[s]);
   }
+  // the query sets this wave works on: set position s holds logical set lid[s] (its slots lid[s]·32 + col, its key
+  // buffers and LDS rows) — wave w's own sets w·QS + s (dealing sets to other waves between groups by their recent
+  // work measured slower: tools/experiments/set_repairing.patch)
+  int lid[QS];
+#pragma unroll
+  for (int s = 0; s < QS; ++s) lid[s] = wave * QS + s;
   half8 bc{};          // CENT: the lane's centroid (fp16, MFMA B operand) ...
   float cslack = 0.0f;  // ... and its slack
-  if constexpr (CENT) {
+  auto setup_centroids = [&]() {
     const int sj = col % QS, mcol0 = QS * (col / QS);
+    int ls = lid[0];
+#pragma unroll
+    for (int s = 1; s < QS; ++s) ls = sj == s ? lid[s] : ls;
     centroid_setup<QS>(emb16, [&](int k) -> int64_t {
-      const int64_t qi = slot_query(block, qslot0 + (wave * QS + sj) * 32 + mcol0 + k, plan.nb, QB);
+      const int64_t qi = slot_query(block, qslot0 + ls * 32 + mcol0 + k, plan.nb, QB);
       return qi < n_active ? (int64_t)active[qi] + q_offset : (int64_t)-1;
     }, bc, cslack);
-  }
+  };
+  if constexpr (CENT) setup_centroids();
   const int nchunks = (int)cdiv(nd, kChunk);  // < 2^31 / 256: chunk arithmetic stays 32-bit (scalar)
   if ((FWAV_TOPK_PRIO & 1) && wave >= W / 2) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half
   // this item's chunk range [c0, c1) (the whole table unless the block is split)
@@ -1651,6 +1667,11 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   if (ngroups > 0) issue_group(0);
 
   int sink = 0;     // ablation builds: keeps the MFMA / fold results of dbg 512/1024 alive
+#ifdef FWAV_TOPK_SETSTATS
+  unsigned long long wait_ticks = 0;
+  const unsigned long long t_all0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  unsigned long long set_ticks[QS] = {};  // SETSTATS: per set position, ticks of level 2 + appends
   int nfired[QS];  // wave-uniform FIFO tail: chunks recorded in sm.fired[group] so far
   ReplayCursor cur[QS];
   int qcnt[QS];    // this lane's entries in its query's two-ended buffer (h = 0: front, h = 1: back)
@@ -1673,7 +1694,13 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       if (STATS) stat_add(12, __builtin_amdgcn_s_memrealtime() - t_b0);
       if (FWAV_TOPK_PRIO & 4) __builtin_amdgcn_s_setprio(0);
+#ifdef FWAV_TOPK_SETSTATS
+      const unsigned long long t_w0 = __builtin_amdgcn_s_memrealtime();
+#endif
       if (!(ABL && (dbg & 16384))) __builtin_amdgcn_s_barrier();  // 16384: own DMA wait, no barrier
+#ifdef FWAV_TOPK_SETSTATS
+      wait_ticks += __builtin_amdgcn_s_memrealtime() - t_w0;
+#endif
       asm volatile("" ::: "memory");
     }
     const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1726,6 +1753,13 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       // memory round trip per batch, as the base geometry's replays) and appended.
       static_for<QS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
+#ifdef FWAV_TOPK_SETSTATS
+        const unsigned long long t_s0 = __builtin_amdgcn_s_memrealtime();
+        struct TickAdd {
+          unsigned long long t0, *dst;
+          __device__ ~TickAdd() { *dst += __builtin_amdgcn_s_memrealtime() - t0; }
+        } tick_add{t_s0, &set_ticks[s]};
+#endif
         using TMask = uint64_t;  // (32-bit masks for ≤ 32-tile groups: 17.15 vs 16.88 ms)
         TMask pm = (TMask)pend[s];
         TMask pass = 0;  // HL: tiles whose s16 passes the set's stream threshold
@@ -1754,7 +1788,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
             } else {
               const int64_t dt = (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32;
               thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT, W>, MODE>(acc[u], thf[s], qcnt[s], kept[s],
-                                                                                 dt, nd, gkeys, sm, wave * QS + s, K,
+                                                                                 dt, nd, gkeys, sm, lid[s], K,
                                                                                  upd[s], stats, sp, emb, qv[s],
                                                                                  &kth[s], share);
             }
@@ -1783,7 +1817,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
               a2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afl[u], b[s], a2, 0, 0, 0);
               const int64_t dt = (int64_t)(cg + (t[u] >> 3)) * kChunk + (t[u] & 7) * 32;
               thf[s] = append_tile<C, STATS, Topk16SmemT<NG, STATS, !CENT, W>, MODE>(a2, thf[s], qcnt[s], kept[s], dt,
-                                                                                 nd, gkeys, sm, wave * QS + s, K,
+                                                                                 nd, gkeys, sm, lid[s], K,
                                                                                  upd[s], stats, sp, emb, qv[s],
                                                                                  &kth[s], share);
             }
@@ -1820,7 +1854,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
         if constexpr (!CENT) {
           if (nfired[s] > cur[s].head || cur[s].rem != 0u)
             thf[s] = replay_window<C, STATS, Topk16SmemT<NG, STATS, !CENT, W>, MODE>(emb16, emb16lo, b[s], bl[s], thf[s],
-                                             qcnt[s], kept[s], cur[s], nfired[s], nd, gkeys, sm, wave * QS + s, K, upd[s],
+                                             qcnt[s], kept[s], cur[s], nfired[s], nd, gkeys, sm, lid[s], K, upd[s],
                                              stats, sp, emb, qv[s], &kth[s], share);
         }
       });
@@ -1833,17 +1867,28 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     }
   }
   const unsigned long long t_final = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
+#ifdef FWAV_TOPK_SETSTATS
+  if (CENT && lane == 0 && blockIdx.x * W + wave < (1 << 16) && blockIdx.x * NG + NG <= (1 << 16)) {
+#pragma unroll
+    for (int s = 0; s < QS; ++s) g_set_ticks[blockIdx.x * NG + lid[s]] += set_ticks[s];
+    g_wave_wait[blockIdx.x * W + wave] = wait_ticks;
+    g_wave_total[blockIdx.x * W + wave] = __builtin_amdgcn_s_memrealtime() - t_all0;
+  }
+#endif
   // the final pass reads the counts from LDS (same wave: program order)
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     if (h == 0)
-      sm.cnt[(wave * QS + s) * 32 + col] = qcnt[s];
+      sm.cnt[lid[s] * 32 + col] = qcnt[s];
     else
-      sm.cnt1[(wave * QS + s) * 32 + col] = qcnt[s];
+      sm.cnt1[lid[s] * 32 + col] = qcnt[s];
   }
 
   for (int l = 0; l < 32 * QS; ++l) {
-    const int qs = wave * QS * 32 + l;
+    int ls = lid[0];
+#pragma unroll
+    for (int s = 1; s < QS; ++s) ls = (l >> 5) == s ? lid[s] : ls;
+    const int qs = ls * 32 + (l & 31);
     const int64_t qq = slot_query(block, qslot0 + qs, plan.nb, QB);
     if (qq >= n_active) continue;
     const int32_t qid = active[qq];
@@ -2490,6 +2535,15 @@ int fwav_debug_cent_stats(unsigned long long* host) {
   (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cent_stats), 4 * sizeof(unsigned long long));
   const unsigned long long z[4] = {0, 0, 0, 0};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_cent_stats), z, sizeof(z));
+  return FWAV_OK;
+}
+#endif
+#ifdef FWAV_TOPK_SETSTATS
+int fwav_debug_set_stats(unsigned long long* sets, unsigned long long* waits, unsigned long long* totals) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(sets, HIP_SYMBOL(g_set_ticks), sizeof(unsigned long long) << 16);
+  (void)hipMemcpyFromSymbol(waits, HIP_SYMBOL(g_wave_wait), sizeof(unsigned long long) << 16);
+  (void)hipMemcpyFromSymbol(totals, HIP_SYMBOL(g_wave_total), sizeof(unsigned long long) << 16);
   return FWAV_OK;
 }
 #endif
