@@ -1670,8 +1670,8 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
 #ifdef FWAV_TOPK_SETSTATS
   unsigned long long wait_ticks = 0;
   const unsigned long long t_all0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long set_ticks[QS] = {};  // per set position, ticks of level 2 + appends
 #endif
-  unsigned long long set_ticks[QS] = {};  // SETSTATS: per set position, ticks of level 2 + appends
   int nfired[QS];  // wave-uniform FIFO tail: chunks recorded in sm.fired[group] so far
   ReplayCursor cur[QS];
   int qcnt[QS];    // this lane's entries in its query's two-ended buffer (h = 0: front, h = 1: back)
