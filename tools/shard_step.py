@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--ranks", default="", help="only these ranks (comma list; default every rank)")
     ap.add_argument("--lags", default="3", help="calls in flight for the pipelined loop (comma list: one column each)")
     ap.add_argument("--tie-order", default="numpy", help="compress_device tie_order (index: no host tie step)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="pipelined loop: consecutive calls alternate over this many HIP streams")
     a = ap.parse_args()
     lags = [int(x) for x in a.lags.split(",")]
     import __graft_entry__
@@ -62,12 +64,14 @@ def main():
             wall = (time.perf_counter() - t0) / a.steps * 1e3
             st = {k: float(np.mean([e[k][0].elapsed_time(e[k][1]) for e in evs])) for k in evs[0]}
             pipes = {}
+            streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(a.streams - 1)]
             for lag in lags:
                 inflight = []
                 t0 = time.perf_counter()
-                for _ in range(a.steps):
-                    inflight.append(engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard,
-                                                           defer_ties=True, tie_order=a.tie_order))
+                for i in range(a.steps):
+                    with torch.cuda.stream(streams[i % len(streams)]):
+                        inflight.append(engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard,
+                                                               defer_ties=True, tie_order=a.tie_order))
                     while len(inflight) > lag:  # calls in flight (bench.py: 3)
                         inflight.pop(0).wait()
                 for x in inflight:
