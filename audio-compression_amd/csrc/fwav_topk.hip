@@ -2358,8 +2358,12 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
       sp, ties)
 #ifdef FWAV_TOPK_EXTSEED
-    if (stats != nullptr && dbg == 0) {
-      if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
+    if (stats != nullptr && (dbg & ~(1 << 18)) == 0) {  // dbg bit 18: the product geometry
+      if (geo == kGeoCent && mode1 == kModeS16)
+        k_sim_topk_f16<k16Cap, false, kModeS16, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
+            emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0,
+            stats, sp, ties);
+      else if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
     } else
 #endif
 #ifdef FWAV_DEBUG_API

@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the timed steps (profiling passes)")
     ap.add_argument("--cpu-workers", default=None, help="CPU baseline search processes (default: sweep)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="HIP streams that consecutive timed calls alternate over (a call's kernels stay on one); "
+                         "default 1 at N = 1, 2 at N > 1")
     return ap.parse_args()
 
 
@@ -226,11 +229,25 @@ def main():
     torch.cuda.synchronize()
 
     phase = {}
+    # --streams S > 1: consecutive calls alternate over S HIP streams, so that one call's search can start on the CUs
+    # the previous call's last workgroups leave idle (each call's kernels stay in order on its own stream)
+    # The N = 1 line keeps one stream so that the search's HIP-event launch time (the roofline) and rocprofv3's
+    # kernel durations measure one launch alone; two streams there measure 17.2 vs 17.8 ms per step
+    # (profiles/r05/bench_streams1.log, bench_streams2.log), with each launch's own duration then stretched by the overlap.
+    n_streams = args.streams if args.streams is not None else (1 if world == 1 else 2)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(max(1, n_streams) - 1)]
+    nstep = [0]
+
+    def call_stream():
+        nstep[0] += 1
+        return streams[(nstep[0] - 1) % len(streams)]
+
     if not sharded:
         def step(ev=None):
             # the host half of numpy-order tie resolution (a few rows per step) overlaps the next step's search;
             # every step's outputs are final (wait()) before the timed region closes
-            r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, events=ev, defer_ties=True)
+            with torch.cuda.stream(call_stream()):
+                r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, events=ev, defer_ties=True)
             step.pending.append(r)
             return r
     else:
@@ -245,8 +262,11 @@ def main():
             # every rank knows the configuration's signal length; per-phase host timings (which synchronise the
             # device at each phase boundary) are taken on extra unpipelined steps after the timed ones
             tm = {} if phases else None
-            h = fdist.compress_sharded_start(sig, tile, K, 1e-4, device=dev, compute=compute, timings=tm,
-                                             n=int(sig_h.size), signal_ready=True)
+            cs = call_stream() if not phases else streams[0]
+            with torch.cuda.stream(cs):
+                h = fdist.compress_sharded_start(sig, tile, K, 1e-4, device=dev, compute=compute, timings=tm,
+                                                 n=int(sig_h.size), signal_ready=True)
+            h["stream"] = cs
             if phases:
                 step.out = fdist.compress_sharded_finish(h)
                 for k_, v in tm.items():
@@ -256,8 +276,12 @@ def main():
                 # gather follows once it is final; every started call is finished inside the timed region (drain)
                 step.inflight.append(h)
                 while len(step.inflight) > LAG:
-                    step.out = fdist.compress_sharded_finish(step.inflight.pop(0))
+                    step.out = finish(step.inflight.pop(0))
             return step.last
+
+        def finish(h):
+            with torch.cuda.stream(h["stream"]):  # the gather on the call's own stream
+                return fdist.compress_sharded_finish(h)
 
         step.inflight = []
 
@@ -270,7 +294,7 @@ def main():
         if not sharded:
             step.pending = []
         while getattr(step, "inflight", None):
-            step.out = fdist.compress_sharded_finish(step.inflight.pop(0))
+            step.out = finish(step.inflight.pop(0))
 
     for _ in range(args.warmup):
         res = step()
@@ -331,7 +355,8 @@ def main():
                                f"top_k={K}, n_ranges={nr}, n_domains={nd}",
                    "tile_size": tile, "top_k": K, "n_ranges": nr, "n_domains": nd,
                    "parallelism": "single GPU" if not sharded else f"ranges sharded x{world} (RCCL broadcast + "
-                                                                  f"gather)"},
+                                                                  f"gather)",
+                   "streams": len(streams)},
         "roofline": {"kernel": f"{TOPK_KERNEL} (fp16 MFMA similarity GEMM pre-filter + streaming exact top-K)",
                      "bound": "mfma", "achieved": achieved_tf, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s",
                      "frac": achieved_tf / F16_MFMA_PEAK_TF, "traffic": traffic, "traffic_source": traffic_src,
@@ -340,7 +365,10 @@ def main():
                                         f"does not execute it all: a centroid bound skips the (tile, query set) pairs "
                                         f"that cannot reach a member's band, so `frac` is an effective rate; the "
                                         f"MFMA work actually executed is `mfma_executed`",
-                     "launch_ms": t_topk * 1e3, "rank": rank},
+                     "launch_ms": t_topk * 1e3, "rank": rank,
+                     **({"note": f"{len(streams)} streams: consecutive launches overlap, so each launch's own duration "
+                                 "(launch_ms) over-states the kernel's time and `frac` under-states it; "
+                                 "roofline_rank_share times the same shard's launch alone"} if len(streams) > 1 else {})},
         "stage_ms": stage_ms,
     }
     sq = sq_summary(args.config) if not sharded else None

@@ -16,11 +16,11 @@ import __graft_entry__
 
 __graft_entry__.build()
 from fwav import engine, synth  # noqa: E402
-from fwav._lib import SIGNATURES, call  # noqa: E402
+from fwav._lib import DEBUG_SIGNATURES, SIGNATURES, call  # noqa: E402
 
 L = C.CDLL(os.path.abspath(sys.argv[1]))
 for n in ("fwav_debug_sim_topk", "fwav_sim_topk_workspace_size"):
-    getattr(L, n).restype, getattr(L, n).argtypes = SIGNATURES[n]
+    getattr(L, n).restype, getattr(L, n).argtypes = {**SIGNATURES, **DEBUG_SIGNATURES}[n]
 sig = torch.from_numpy(synth.noise(60.0, 44100)).cuda()
 r = engine.compress_device(sig, 2048, 64, keep_intermediates=True)
 torch.cuda.synchronize()
@@ -42,11 +42,19 @@ E = emb.view(nd, 16)
 ref = None
 for S in [0] + [int(x) for x in sys.argv[2:]]:
     seeds = torch.full((nr,), -float("inf"), device="cuda")
-    if S < 0:  # ideal: the exact K-th best score of every query (from the search's own candidates), minus 3δ
+    if -1000 <= S < 0:  # ideal: the exact K-th best score of every query (from the search's own candidates), minus 3δ
         # (S = -1), or minus (-S)/1000 more (S = -20: 0.020 below the ideal seed)
         kth = r.cand.view(nr, 64)[:, 63].long()
         seeds = ((E[:nr].double() * E[kth].double()).sum(1) - 3 * 2.0e-3 - (0 if S == -1 else -S / 1000.0)).float()
-    if S > 0:
+    if S < -1000:
+        # one global seed g = (-S - 1000) / 1000 (e.g. -2870: 1.870), capped per query at its ideal seed so that it
+        # stays a valid lower bound: the time a global seed would take if its misses were free
+        kth = r.cand.view(nr, 64)[:, 63].long()
+        ideal = ((E[:nr].double() * E[kth].double()).sum(1) - 3 * 2.0e-3).float()
+        seeds = torch.clamp(ideal, max=(-S - 1000) / 1000.0)
+        print(f"global seed {(-S - 1000) / 1000.0:.3f}: {(ideal < (-S - 1000) / 1000.0).float().mean().item():.4%} "
+              "of the queries below it", flush=True)
+    elif S > 0:
         samp = torch.linspace(0, nd - 1, S, device="cuda").long()
         Es = E[samp].double()
         for a in range(0, nr, 32768):
@@ -59,7 +67,8 @@ for S in [0] + [int(x) for x in sys.argv[2:]]:
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         rc = L.fwav_debug_sim_topk(emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, 0,
-                                   64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), 0, seeds.data_ptr(), st)
+                                   64, cand.data_ptr(), wsk.data_ptr(), wsk.numel(), int(os.environ.get("AB_DBG", "0")),
+                                   seeds.data_ptr(), st)
         e1.record()
         torch.cuda.synchronize()
         assert rc == 0

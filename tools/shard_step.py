@@ -65,23 +65,31 @@ def main():
             st = {k: float(np.mean([e[k][0].elapsed_time(e[k][1]) for e in evs])) for k in evs[0]}
             pipes = {}
             streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(a.streams - 1)]
+            host = {}
             for lag in lags:
                 inflight = []
+                t_call = t_wait = 0.0
                 t0 = time.perf_counter()
                 for i in range(a.steps):
+                    ta = time.perf_counter()
                     with torch.cuda.stream(streams[i % len(streams)]):
                         inflight.append(engine.compress_device(sig, tile, K, energy_thresh=1e-4, shard=shard,
                                                                defer_ties=True, tie_order=a.tie_order))
+                    tb = time.perf_counter()
                     while len(inflight) > lag:  # calls in flight (bench.py: 3)
                         inflight.pop(0).wait()
+                    t_call += tb - ta
+                    t_wait += time.perf_counter() - tb
                 for x in inflight:
                     x.wait()
                 torch.cuda.synchronize()
                 pipes[lag] = (time.perf_counter() - t0) / a.steps * 1e3
+                # host ms per call inside compress_device (launch + any host synchronisation) and blocked in wait()
+                host[lag] = {"call_ms": t_call / a.steps * 1e3, "wait_ms": t_wait / a.steps * 1e3}
             pipe = pipes[lags[0]]
             per.append({"rank": rank, "ranges": r.shard[1] - r.shard[0], "tie_rows": r.n_resolved,
                         "wall_ms_sync": wall, "wall_ms_pipelined": pipe,
-                        "wall_ms_pipelined_by_lag": pipes, "stage_ms": st})
+                        "wall_ms_pipelined_by_lag": pipes, "host_by_lag": host, "stage_ms": st})
         out[N] = {"max_wall_ms_sync": max(p["wall_ms_sync"] for p in per),
                   "max_wall_ms_pipelined": max(p["wall_ms_pipelined"] for p in per), "ranks": per}
         print(N, json.dumps(out[N]), flush=True)

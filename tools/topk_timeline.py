@@ -1,5 +1,5 @@
 """Workgroup timeline of the similarity search (dbg 4096): how busy the GPU's workgroup slots are over time.
-usage: [PLAN=rt:P] python tools/topk_timeline.py [dbg_extra]   (prints occupancy profile + the tail's share of the kernel)"""
+usage: [PLAN=rt:P] [AB_NQ=n] python tools/topk_timeline.py [dbg_extra]   (AB_NQ: the first n queries only)   (prints occupancy profile + the tail's share of the kernel)"""
 import os as _os_dbg
 _os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
@@ -31,6 +31,7 @@ ws = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 call("fwav_pool_embed", sig.data_ptr(), sig.numel(), 2048, 8, 2, tab.data_ptr(), pool.data_ptr(), emb.data_ptr(),
      emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+nr = int(os.environ.get("AB_NQ", nr))
 active = torch.arange(nr, dtype=torch.int32, device="cuda")
 n_active = torch.tensor([nr], dtype=torch.int32, device="cuda")
 cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
