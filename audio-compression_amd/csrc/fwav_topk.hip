@@ -32,6 +32,7 @@
 // to its top K and θ set to the K-th score.  Domains stream in increasing index order, so a later domain whose
 // score equals θ can never displace an earlier one: strict '>' is exact.
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 #include "fwav_common.h"
 #include "../../include/fwav.h"
@@ -45,7 +46,8 @@
     defined(FWAV_TOPK_CENT_MINQ) || defined(FWAV_TOPK_CG) || defined(FWAV_TOPK_CHAINS) || defined(FWAV_TOPK_CPDBL) || \
     defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || defined(FWAV_TOPK_CVACC) || defined(FWAV_TOPK_CW) || \
     defined(FWAV_TOPK_CWPE) || defined(FWAV_TOPK_DEBUG) || defined(FWAV_TOPK_DELTA) || defined(FWAV_TOPK_EXGROW) || \
-    defined(FWAV_TOPK_EXTSEED) || defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_G) || \
+    defined(FWAV_TOPK_EXTSEED) || defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_FLOOR) || \
+    defined(FWAV_TOPK_FLOOR_MIND) || defined(FWAV_TOPK_FLOOR_MINQ) || defined(FWAV_TOPK_G) || \
     defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
     defined(FWAV_TOPK_INTERLEAVE) || defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_MERGE_WG) || \
     defined(FWAV_TOPK_MSKIP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
@@ -568,6 +570,24 @@ struct TopkPlan {
   // the item of table piece p of split block b
   __host__ __device__ int64_t item_of(int64_t b, int p) const { return pm ? F + (int64_t)p * R + (b - F) : F + (b - F) * P + p; }
 };
+// Speculative band floor of a first pass (launch_topk): *key = f2key of a filter floor f on the pass's own score scale
+// (s16 or shl; 0 = no floor).  Every query's band limit starts at f, so the pass skips the rise of its limit from the
+// seed; a query whose exact K-th score does not clear f + 2δ (δ ≥ |s16 − s32|, ≥ |shl − s32|: then every exact
+// top-K member had a filter score above f, and the result is exact) is listed in miss[0 .. *n_miss) for the
+// floor-free second pass instead of being emitted.
+struct FloorCtl {
+  const uint32_t* key;
+  int32_t* miss;
+  int32_t* n_miss;
+};
+// Whole wave: true (and the query listed for the second pass) when the floor may have cut a member of its top K:
+// fewer than K band entries, or a K-th exact score (kth: key) not above f + 2δ.
+__device__ __forceinline__ bool floor_miss(uint32_t fkey, const FloorCtl& fl, int n, int K, uint64_t kth, int32_t qid) {
+  if (fkey == 0u) return false;
+  const bool miss = !(n >= K && key_score(kth) > key2f(fkey) + 2.0f * kF16Delta);
+  if (miss && (threadIdx.x & 63) == 0) fl.miss[atomicAdd(fl.n_miss, 1)] = qid;
+  return miss;
+}
 __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, int qb) {
   TopkPlan pl;
   pl.qb = qb;
@@ -749,7 +769,8 @@ __device__ __forceinline__ void compact16_s16(uint64_t* __restrict__ kq, int n0,
 template <int C, int E, class SM>
 __device__ __forceinline__ void compact16_e(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
                                             const float* __restrict__ emb, int32_t* __restrict__ out,
-                                            const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid) {
+                                            const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid,
+                                            uint32_t fkey, const FloorCtl& fl) {
   const int lane = threadIdx.x & 63;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int n0 = sm.cnt[ql];
@@ -798,6 +819,8 @@ __device__ __forceinline__ void compact16_e(uint64_t* __restrict__ kq, SM& sm, i
 #pragma unroll
   for (int j = 0; j < E; ++j)
     if (j == ((K - 1) >> 6)) kth = __shfl(v[j], (K - 1) & 63);
+  // a speculative floor that may have cut a member: the query goes to the second pass, nothing is emitted here
+  if (sm.ovf[ql] == 0 && floor_miss(fkey, fl, n, K, kth, qid)) return;
   const uint32_t tv = sm.tie[ql];
   const int tf = tie_flags<E>(v, n, K) | (tv != 0u && n >= K && key2f(tv) == key_score(kth) ? 2 : 0);
   // the band of the S16 / HL modes holds every domain within the band margin of the K-th score, so the K-th's whole
@@ -817,12 +840,13 @@ __device__ __forceinline__ void compact16_e(uint64_t* __restrict__ kq, SM& sm, i
 template <int C, class SM>
 __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
                                           const float* __restrict__ emb, int32_t* __restrict__ out,
-                                          const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid) {
+                                          const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid,
+                                          uint32_t fkey, const FloorCtl& fl) {
   const int n = __builtin_amdgcn_readfirstlane(sm.cnt[ql] + sm.cnt1[ql]);
   if (FWAV_TOPK_SMALLSORT && C > 128 && n <= 128)
-    compact16_e<C, 2, SM>(kq, sm, ql, K, emb, out, sp, ties, qid);
+    compact16_e<C, 2, SM>(kq, sm, ql, K, emb, out, sp, ties, qid, fkey, fl);
   else
-    compact16_e<C, C / 64, SM>(kq, sm, ql, K, emb, out, sp, ties, qid);
+    compact16_e<C, C / 64, SM>(kq, sm, ql, K, emb, out, sp, ties, qid, fkey, fl);
 }
 
 // End of a table piece (split block): no rescoring and no sort here — the piece keeps the entries of its band whose
@@ -1497,7 +1521,8 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
                                                                 const uint32_t* __restrict__ seeds_in,
                                                                 float seed_shift, int plan_rt,
                                                                 int plan_p, int dbg, unsigned long long* gstats,
-                                                                SgemvSplit sp, int32_t* __restrict__ ties) {
+                                                                SgemvSplit sp, int32_t* __restrict__ ties,
+                                                                FloorCtl fl) {
   constexpr bool EX = MODE == kModeEX;
   constexpr bool HL = MODE == kModeHL;
   constexpr int NG = W * QS;  // query groups of 32 per workgroup; wave w owns groups w·QS .. w·QS + QS − 1
@@ -1611,6 +1636,13 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
 #pragma unroll
     for (int s = 0; s < QS; ++s)
       if (upd[s]) thf[s] = fmaxf(thf[s], inseed[s]);
+  }
+  // a first pass's speculative floor (FloorCtl): every band limit starts there
+  const uint32_t fkey = (!EX && fl.key != nullptr) ? __builtin_amdgcn_readfirstlane(*fl.key) : 0u;
+  if (fkey != 0u) {
+#pragma unroll
+    for (int s = 0; s < QS; ++s)
+      if (upd[s]) thf[s] = fmaxf(thf[s], key2f(fkey));
   }
   // the query sets this wave works on: set position s holds logical set lid[s] (its slots lid[s]·32 + col, its key
   // buffers and LDS rows) — wave w's own sets w·QS + s (dealing sets to other waves between groups by their recent
@@ -1899,7 +1931,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       continue;
     }
     // exact f32 rescoring of the kept band + sort
-    compact16<C>(kq, sm, qs, K, emb, cand + (int64_t)qid * K, sp, ties, qid);
+    compact16<C>(kq, sm, qs, K, emb, cand + (int64_t)qid * K, sp, ties, qid, fkey, fl);
     // overflowed: listed for the exact-mode relaunch with its band limit as the seed (same list position)
     if (lane == 0 && sm.ovf[qs]) {
       const int pos = atomicAdd(n_ovf, 1);
@@ -1940,7 +1972,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
 template <int E>
 __device__ __forceinline__ void merge_band(const uint64_t* __restrict__ sw, int mb, int K, const float* __restrict__ emb,
                                            int64_t qrow, const SgemvSplit& sp, int32_t* __restrict__ ties, int32_t qid,
-                                           int32_t* __restrict__ out) {
+                                           int32_t* __restrict__ out, uint32_t fkey, const FloorCtl& fl) {
   const int lane = threadIdx.x & 63;
   uint64_t v[E];
 #pragma unroll
@@ -1969,6 +2001,13 @@ __device__ __forceinline__ void merge_band(const uint64_t* __restrict__ sw, int 
     }
   }
   wave_sort_desc<E>(v);
+  if (fkey != 0u) {
+    uint64_t kth = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (j == ((K - 1) >> 6)) kth = __shfl(v[j], (K - 1) & 63);
+    if (floor_miss(fkey, fl, mb, K, kth, qid)) return;
+  }
   record_tie<E>(ties, qid, tie_flags<E>(v, mb, K), v, mb, K, true);
 #pragma unroll
   for (int j = 0; j < E; ++j) {
@@ -1984,7 +2023,8 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
                                             int n_active, int K, int32_t* __restrict__ cand,
                                             int32_t* __restrict__ ovf_list, int32_t* __restrict__ n_ovf,
                                             const uint32_t* __restrict__ share, const float* __restrict__ emb,
-                                            int64_t q_offset, const SgemvSplit& sp, int32_t* __restrict__ ties);
+                                            int64_t q_offset, const SgemvSplit& sp, int32_t* __restrict__ ties,
+                                            uint32_t fkey, const FloorCtl& fl);
 
 template <int C, int QB, bool HL>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
@@ -1993,8 +2033,9 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
                                                       int K, int32_t* __restrict__ cand, int32_t* __restrict__ ovf_list,
                                                       int32_t* __restrict__ n_ovf, const uint32_t* __restrict__ share,
                                                       const float* __restrict__ emb, int64_t q_offset, SgemvSplit sp,
-                                                      int32_t* __restrict__ ties) {
+                                                      int32_t* __restrict__ ties, FloorCtl fl) {
   const int n_active = *n_active_p;
+  const uint32_t fkey = fl.key != nullptr ? __builtin_amdgcn_readfirstlane(*fl.key) : 0u;
   const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
   if (plan.R == 0 || plan.halves) return;
   const int lane = threadIdx.x & 63;
@@ -2006,7 +2047,7 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   // reading the pieces' bands, not by dispatch (profiles/r05/merge_sq_cfg2.log)
   for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < plan.R * QB; w += (int64_t)gridDim.x * 4)
     merge_query<C, QB, HL>(plan, w, lane, sw, gkeys_all, active, n_active, K, cand, ovf_list, n_ovf, share, emb,
-                           q_offset, sp, ties);
+                           q_offset, sp, ties, fkey, fl);
 }
 
 // One split-block query w of k_merge_pieces (whole wave; sw: the wave's LDS row).
@@ -2016,7 +2057,8 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
                                             int n_active, int K, int32_t* __restrict__ cand,
                                             int32_t* __restrict__ ovf_list, int32_t* __restrict__ n_ovf,
                                             const uint32_t* __restrict__ share, const float* __restrict__ emb,
-                                            int64_t q_offset, const SgemvSplit& sp, int32_t* __restrict__ ties) {
+                                            int64_t q_offset, const SgemvSplit& sp, int32_t* __restrict__ ties,
+                                            uint32_t fkey, const FloorCtl& fl) {
   constexpr int E = C / 64;
   const int64_t block = plan.F + w / QB;
   const int ql = (int)(w % QB);
@@ -2114,9 +2156,9 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
   }
   // same wave: its own ds_writes are ordered before merge_band's reads
   if (FWAV_TOPK_SMALLSORT && C > 128 && mb <= 128)
-    merge_band<2>(sw, mb, K, emb, (int64_t)qid + q_offset, sp, ties, qid, cand + (int64_t)qid * K);
+    merge_band<2>(sw, mb, K, emb, (int64_t)qid + q_offset, sp, ties, qid, cand + (int64_t)qid * K, fkey, fl);
   else
-    merge_band<E>(sw, mb, K, emb, (int64_t)qid + q_offset, sp, ties, qid, cand + (int64_t)qid * K);
+    merge_band<E>(sw, mb, K, emb, (int64_t)qid + q_offset, sp, ties, qid, cand + (int64_t)qid * K, fkey, fl);
 }
 
 // Host-side plan: default policy from the device's workgroup slots, or a diagnostic override.
@@ -2278,11 +2320,149 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
   const int64_t pmax = cdiv(nd, kChunk) / 16;
   if (P > pmax) P = (int)(pmax > 1 ? pmax : 1);
 }
+// ---------------------------------------------------------------------------------------- speculative floor
+// A first pass of at least FWAV_TOPK_FLOOR_MINQ queries over at least FWAV_TOPK_FLOOR_MIND domains starts every band
+// limit at a floor guessed from kFloorPilots pilot queries (FloorCtl); the queries it cuts are searched again.
+// Measured (tools/seed_ab.py, profiles/r05/seed_floor_cfg2.log): cfg2's search 17.01 ms unseeded, 15.27 / 14.71 /
+// 14.12 ms with one floor of 1.80 / 1.85 / 1.88 for every query (0.05 / 0.38 / 1.7 % of the queries below it, their
+// misses not counted), 12.20 ms with each query's own exact K-th score.
+#ifndef FWAV_TOPK_FLOOR
+#define FWAV_TOPK_FLOOR 1
+#endif
+#ifndef FWAV_TOPK_FLOOR_MINQ
+#define FWAV_TOPK_FLOOR_MINQ 32768
+#endif
+#ifndef FWAV_TOPK_FLOOR_MIND
+#define FWAV_TOPK_FLOOR_MIND 65536
+#endif
+constexpr int kFloorPilots = 512;  // pilot queries (evenly spaced over the active list), one k_floor_reduce thread each
+constexpr int kFloorWG = 256;      // k_floor_pilot workgroups, each over a 1/kFloorWG slice of the sampled domains
+constexpr int kFloorJ = 4;         // the pilot's estimate: its j-th best score over every (K/j)-th domain ≈ its K-th
+constexpr int kFloorSplit = 32;    // second pass: blocks split into kMaxPieces table pieces (the rest whole-table)
+#ifdef FWAV_DEBUG_API
+static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 forced value, 2 pilot at any size
+static uint32_t g_floor_key = 0u;
+#else
+constexpr int g_floor_mode = -1;
+constexpr uint32_t g_floor_key = 0u;
+#endif
+static int floor_mode() { return FWAV_TOPK_FLOOR ? g_floor_mode : 0; }
+// second-pass plan (base geometry) for a miss list of at most max_q queries
+static void floor_plan(int64_t max_q, int& rt, int& P) {
+  (void)max_q;
+  rt = kFloorSplit;
+  P = kMaxPieces;
+}
+
+// Each pilot p (of kFloorPilots, 2 per thread) at active position p·n/kFloorPilots: its kFloorJ best f32 scores over
+// the sampled domains m·stride of this workgroup's slice, to scratch[(block·kFloorPilots + p)·kFloorJ + i].  The
+// slice's domain rows are staged in LDS 256 at a time.  (A guess only: no reference order needed.)
+__global__ __launch_bounds__(256) void k_floor_pilot(const float* __restrict__ emb, int64_t nd,
+                                                     const int32_t* __restrict__ active,
+                                                     const int32_t* __restrict__ n_active_p, int64_t q_offset,
+                                                     int stride, float* __restrict__ scratch) {
+  __shared__ float4 rows[256][4];
+  const int na = *n_active_p;
+  const int64_t M = (nd + stride - 1) / stride;
+  const int64_t m0 = M * blockIdx.x / gridDim.x, m1 = M * (blockIdx.x + 1) / gridDim.x;
+  float q[2][16], top[2][kFloorJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = threadIdx.x * 2 + i;
+    const int64_t pos = na > 0 ? (int64_t)p * na / kFloorPilots : 0;
+    const int64_t row = na > 0 ? (int64_t)active[pos] + q_offset : 0;
+    const float4* qp = reinterpret_cast<const float4*>(emb + row * 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = qp[k];
+      q[i][4 * k] = v.x; q[i][4 * k + 1] = v.y; q[i][4 * k + 2] = v.z; q[i][4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < kFloorJ; ++k) top[i][k] = -INFINITY;
+  }
+  for (int64_t mb = m0; mb < m1; mb += 256) {
+    const int nr = (int)min<int64_t>(256, m1 - mb);
+    __syncthreads();
+    if ((int)threadIdx.x < nr) {
+      const float4* rp = reinterpret_cast<const float4*>(emb + (mb + threadIdx.x) * stride * 16);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) rows[threadIdx.x][k] = rp[k];
+    }
+    __syncthreads();
+    for (int r = 0; r < nr; ++r) {
+      float4 d[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[k] = rows[r][k];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float x = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          x += q[i][4 * k] * d[k].x + q[i][4 * k + 1] * d[k].y + q[i][4 * k + 2] * d[k].z + q[i][4 * k + 3] * d[k].w;
+        // sorted insertion into the pilot's top kFloorJ (descending)
+#pragma unroll
+        for (int k = 0; k < kFloorJ; ++k) {
+          const float hi = fmaxf(top[i][k], x);
+          x = fminf(top[i][k], x);
+          top[i][k] = hi;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < kFloorJ; ++k)
+      scratch[((int64_t)blockIdx.x * kFloorPilots + threadIdx.x * 2 + i) * kFloorJ + k] = top[i][k];
+}
+
+// Thread p: pilot p's j-th best over all slices (its estimate of its K-th score); the floor is the smallest estimate
+// (key in f2key order; 0 = no floor: fewer than min_q active queries, or no finite estimate).
+__global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __restrict__ scratch, int nwg, int j,
+                                                               const int32_t* __restrict__ n_active_p, int min_q,
+                                                               uint32_t* __restrict__ floor_key) {
+  __shared__ float red[kFloorPilots / 64];
+  const int p = threadIdx.x;
+  float top[kFloorJ];
+#pragma unroll
+  for (int k = 0; k < kFloorJ; ++k) top[k] = -INFINITY;
+  for (int b = 0; b < nwg; ++b) {
+#pragma unroll
+    for (int i = 0; i < kFloorJ; ++i) {
+      float x = scratch[((int64_t)b * kFloorPilots + p) * kFloorJ + i];
+#pragma unroll
+      for (int k = 0; k < kFloorJ; ++k) {
+        const float hi = fmaxf(top[k], x);
+        x = fminf(top[k], x);
+        top[k] = hi;
+      }
+    }
+  }
+  float e = top[0];
+#pragma unroll
+  for (int k = 1; k < kFloorJ; ++k) e = k == j - 1 ? top[k] : e;
+  for (int off = 32; off > 0; off >>= 1) e = fminf(e, __shfl_xor(e, off));
+  if ((p & 63) == 0) red[p >> 6] = e;
+  __syncthreads();
+  if (p == 0) {
+    float m = red[0];
+    for (int w = 1; w < kFloorPilots / 64; ++w) m = fminf(m, red[w]);
+    const int na = *n_active_p;
+    floor_key[0] = (na >= min_q && na > 0 && m > -INFINITY && m < INFINITY) ? f2key(m) : 0u;
+  }
+}
+
 // Key-buffer bytes: enough for the first pass in either geometry (a diagnostic override may switch it between the
-// size query and the launch) and for the relaunches' base plan.
+// size query and the launch), for the relaunches' base plan and for the floor's second pass.
 static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
   const int64_t q = max_q > 0 ? max_q : 1;
   size_t items_q = (size_t)make_plan(q, 0, 1, k16QB).items() * k16QB;
+  {
+    int rt2, P2;
+    floor_plan(q, rt2, P2);
+    const size_t n2 = (size_t)make_plan(q, rt2, P2, k16QB).items() * k16QB;
+    items_q = n2 > items_q ? n2 : items_q;
+  }
   for (int geo = 0; geo < 4; ++geo) {
     int rt, P;
     host_plan_for(q, nd, geo, rt, P);
@@ -2332,86 +2512,117 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     constexpr bool stats_first = false;  // counter / ablation launches: debug library only
     (void)dbg;
 #endif
-    // counter (STATS) builds of the first pass exist in the base geometry only
     // counter builds run the base geometry, or with dbg bit 18 the product's own (centroid) geometry
     const int geo = stats_first && !(dbg & (1 << 18)) ? kGeoBase : first_geometry(nd, max_q);
-    const bool wide = geo == kGeoWide;
-    int rt, P;
-    host_plan_for(max_q, nd, geo, rt, P);
-    const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(geo));
-    if (pl.R > 0 && !pl.halves) (void)hipMemsetAsync(share, 0, (size_t)q1 * sizeof(uint32_t), st);
     const int mode1 = first_mode(nd);
+    // workspace after the two overflow lists: the floor's miss list (list[q], count), the floor key, the pilot scores
+    int32_t* miss = const_cast<int32_t*>(reinterpret_cast<const int32_t*>(seeds1 + q1));
+    int32_t* n_miss = miss + q1;
+    uint32_t* floor_key = reinterpret_cast<uint32_t*>(n_miss + 1);
+    float* pilot = reinterpret_cast<float*>(floor_key + 1);
+    // One first pass (search + merge of split blocks) over act[0 .. *nact) in geometry g with plan (rt, P) and floor
+    // fl; `diag`: the debug library's counter / ablation launches may replace the search
+    auto first_pass = [&](const int32_t* act, const int32_t* nact, int g, int rt, int P, FloorCtl fl, bool diag) {
+      const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(g));
+      if (pl.R > 0 && !pl.halves) (void)hipMemsetAsync(share, 0, (size_t)q1 * sizeof(uint32_t), st);
 #define FWAV_FIRST(MODE_, STATS_, DBG_, ST_)                                                                    \
-  k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, 0, st>>>(                  \
-      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, DBG_, ST_,  \
-      sp, ties)
-#define FWAV_FIRST_WIDE(MODE_)                                                                                   \
-  k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG, 1><<<pl.items(), 64 * kWideW, 0, st>>>(                    \
-      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
-      sp, ties)
-#define FWAV_FIRST_CENTW(MODE_)                                                                                  \
-  k_sim_topk_f16<k16Cap, false, MODE_, kWideW, kWideG, kCentWideQS, true><<<pl.items(), 64 * kWideW, 0, st>>>(    \
-      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
-      sp, ties)
-#define FWAV_FIRST_CENT(MODE_)                                                                                   \
-  k_sim_topk_f16<k16Cap, false, MODE_, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(        \
-      emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
-      sp, ties)
+  k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, 0, st>>>(                                  \
+      emb16, emb, nd, act, nact, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, DBG_, ST_,  \
+      sp, ties, fl)
+#define FWAV_FIRST_GEO(MODE_, W_, G_, QS_, CENT_)                                                               \
+  k_sim_topk_f16<k16Cap, false, MODE_, W_, G_, QS_, CENT_><<<pl.items(), 64 * W_, 0, st>>>(                     \
+      emb16, emb, nd, act, nact, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0, nullptr, \
+      sp, ties, fl)
+      bool done = false;
+      (void)diag;
 #ifdef FWAV_TOPK_EXTSEED
-    if (stats != nullptr && (dbg & ~(1 << 18)) == 0) {  // dbg bit 18: the product geometry
-      if (geo == kGeoCent && mode1 == kModeS16)
-        k_sim_topk_f16<k16Cap, false, kModeS16, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
-            emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0,
-            stats, sp, ties);
-      else if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
-    } else
+      if (diag && stats != nullptr && (dbg & ~(1 << 18)) == 0) {  // dbg bit 18: the product geometry
+        if (g == kGeoCent && mode1 == kModeS16)
+          k_sim_topk_f16<k16Cap, false, kModeS16, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
+              emb16, emb, nd, act, nact, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0,
+              stats, sp, ties, fl);
+        else if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
+        done = true;
+      }
 #endif
 #ifdef FWAV_DEBUG_API
-    if (stats_first && geo == kGeoCent) {
-      if (mode1 == kModeHL)
-        k_sim_topk_f16<k16Cap, true, kModeHL, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
-            emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P,
-            dbg & 65535, stats, sp, ties);
-      else
-        k_sim_topk_f16<k16Cap, true, kModeS16, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
-            emb16, emb, nd, active, n_active, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P,
-            dbg & 65535, stats, sp, ties);
-    } else if (stats_first) {
-      if (mode1 == kModeHL) FWAV_FIRST(kModeHL, true, dbg & 65535, stats);
-      else FWAV_FIRST(kModeS16, true, dbg & 65535, stats);
-    } else
+      if (!done && diag && stats_first && g == kGeoCent) {
+        if (mode1 == kModeHL)
+          k_sim_topk_f16<k16Cap, true, kModeHL, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
+              emb16, emb, nd, act, nact, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P,
+              dbg & 65535, stats, sp, ties, fl);
+        else
+          k_sim_topk_f16<k16Cap, true, kModeS16, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
+              emb16, emb, nd, act, nact, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P,
+              dbg & 65535, stats, sp, ties, fl);
+        done = true;
+      } else if (!done && diag && stats_first) {
+        if (mode1 == kModeHL) FWAV_FIRST(kModeHL, true, dbg & 65535, stats);
+        else FWAV_FIRST(kModeS16, true, dbg & 65535, stats);
+        done = true;
+      }
 #endif
-    if (wide) {
-      if (mode1 == kModeHL) FWAV_FIRST_WIDE(kModeHL); else FWAV_FIRST_WIDE(kModeS16);
-    } else if (geo == kGeoCent) {
-      if (mode1 == kModeHL) FWAV_FIRST_CENT(kModeHL); else FWAV_FIRST_CENT(kModeS16);
-    } else if (geo == kGeoCentWide) {
-      if (mode1 == kModeHL) FWAV_FIRST_CENTW(kModeHL); else FWAV_FIRST_CENTW(kModeS16);
-    } else {
-      if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, nullptr); else FWAV_FIRST(kModeS16, false, 0, nullptr);
-    }
+      if (!done) {
+        if (g == kGeoWide) {
+          if (mode1 == kModeHL) FWAV_FIRST_GEO(kModeHL, kWideW, kWideG, 1, false);
+          else FWAV_FIRST_GEO(kModeS16, kWideW, kWideG, 1, false);
+        } else if (g == kGeoCent) {
+          if (mode1 == kModeHL) FWAV_FIRST_GEO(kModeHL, kCentW, kCentG, kCentQS, true);
+          else FWAV_FIRST_GEO(kModeS16, kCentW, kCentG, kCentQS, true);
+        } else if (g == kGeoCentWide) {
+          if (mode1 == kModeHL) FWAV_FIRST_GEO(kModeHL, kWideW, kWideG, kCentWideQS, true);
+          else FWAV_FIRST_GEO(kModeS16, kWideW, kWideG, kCentWideQS, true);
+        } else {
+          if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, nullptr); else FWAV_FIRST(kModeS16, false, 0, nullptr);
+        }
+      }
 #undef FWAV_FIRST
-#undef FWAV_FIRST_WIDE
-#undef FWAV_FIRST_CENT
-#undef FWAV_FIRST_CENTW
-    if (pl.R > 0) {
-      // persistent merge waves: ≈ 6 per SIMD (its occupancy), each looping over split-block queries
-      int cus, per_cu;
-      topk_device_slots(geo, cus, per_cu);
-      const int64_t mgrid_cap = (int64_t)cus * FWAV_TOPK_MERGE_WG;
+#undef FWAV_FIRST_GEO
+      if (pl.R > 0) {
+        // persistent merge waves: ≈ 6 per SIMD (its occupancy), each looping over split-block queries
+        int cus, per_cu;
+        topk_device_slots(g, cus, per_cu);
+        const int64_t mgrid_cap = (int64_t)cus * FWAV_TOPK_MERGE_WG;
 #define FWAV_MERGE(QB_, HL_)                                                                                    \
   k_merge_pieces<k16Cap, QB_, HL_><<<std::min<int64_t>(cdiv(pl.R * QB_, 4), mgrid_cap), 256, 0, st>>>(          \
-      gkeys, active, n_active, rt, P, K, cand, ovf1, n_ovf1, share, emb, q_offset, sp, ties)
-      if (wide) {
-        if (mode1 == kModeHL) FWAV_MERGE(kWideQB, true); else FWAV_MERGE(kWideQB, false);
-      } else if (geo == kGeoCent) {
-        if (mode1 == kModeHL) FWAV_MERGE(kCentQB, true); else FWAV_MERGE(kCentQB, false);
-      } else if (geo == kGeoCentWide) {
-        if (mode1 == kModeHL) FWAV_MERGE(kCentWideQB, true); else FWAV_MERGE(kCentWideQB, false);
-      } else {
-        if (mode1 == kModeHL) FWAV_MERGE(k16QB, true); else FWAV_MERGE(k16QB, false);
-      }
+      gkeys, act, nact, rt, P, K, cand, ovf1, n_ovf1, share, emb, q_offset, sp, ties, fl)
+        if (g == kGeoWide) {
+          if (mode1 == kModeHL) FWAV_MERGE(kWideQB, true); else FWAV_MERGE(kWideQB, false);
+        } else if (g == kGeoCent) {
+          if (mode1 == kModeHL) FWAV_MERGE(kCentQB, true); else FWAV_MERGE(kCentQB, false);
+        } else if (g == kGeoCentWide) {
+          if (mode1 == kModeHL) FWAV_MERGE(kCentWideQB, true); else FWAV_MERGE(kCentWideQB, false);
+        } else {
+          if (mode1 == kModeHL) FWAV_MERGE(k16QB, true); else FWAV_MERGE(k16QB, false);
+        }
 #undef FWAV_MERGE
+      }
+    };
+    int rt, P;
+    host_plan_for(max_q, nd, geo, rt, P);
+    // Speculative floor (FloorCtl): from the exact scores of kFloorPilots evenly spaced queries against every
+    // stride-th domain (k_floor_pilot), a guess at the lowest K-th score of the search; queries it cuts are searched
+    // again without it (the second pass: base geometry, its blocks split in kFloorPieces table pieces).
+    const int fmode = floor_mode();
+    const bool use_floor = !stats_first && fmode != 0 && K <= 64 &&
+                           (fmode > 0 || (max_q >= (int64_t)FWAV_TOPK_FLOOR_MINQ && nd >= (int64_t)FWAV_TOPK_FLOOR_MIND));
+    FloorCtl fl{nullptr, nullptr, nullptr};
+    if (use_floor) {
+      (void)hipMemsetAsync(n_miss, 0, sizeof(int32_t), st);
+      if (fmode == 1) {  // debug: a forced floor value
+        (void)hipMemsetD32Async((hipDeviceptr_t)floor_key, (int)g_floor_key, 1, st);
+      } else {
+        const int j = K < kFloorJ ? K : kFloorJ, stride = K / j;
+        k_floor_pilot<<<kFloorWG, 256, 0, st>>>(emb, nd, active, n_active, q_offset, stride, pilot);
+        k_floor_reduce<<<1, kFloorPilots, 0, st>>>(pilot, kFloorWG, j, n_active, FWAV_TOPK_FLOOR_MINQ, floor_key);
+      }
+      fl = FloorCtl{floor_key, miss, n_miss};
+    }
+    first_pass(active, n_active, geo, rt, P, fl, true);
+    if (use_floor) {
+      int rt2, P2;
+      floor_plan(max_q, rt2, P2);
+      first_pass(miss, n_miss, kGeoBase, rt2, P2, FloorCtl{nullptr, nullptr, nullptr}, false);
     }
     // Queries whose band overflowed the buffer (large groups of equal or nearly equal scores) are searched again by
     // the same kernel in a narrower mode, on the device-side overflow list (no host sync; a relaunch exits at once
@@ -2424,7 +2635,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     if (mode1 == kModeS16) {
       k_sim_topk_f16<k16Cap, false, kModeHL><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, ovf1, n_ovf1, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, seeds1, kStreamMargin, 0, 1, 0,
-          nullptr, sp, ties);
+          nullptr, sp, ties, FloorCtl{nullptr, nullptr, nullptr});
       ex_in = ovf2;
       ex_n = n_ovf2;
       ex_seeds = seeds2;
@@ -2433,12 +2644,12 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     if (stats != nullptr && (dbg & (1 << 17)))  // diagnostic: counters of the exact-mode relaunch only
       k_sim_topk_f16<k16Cap, true, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, ex_seeds, kStreamMargin, 0, 1, 0,
-          stats, sp, ties);
+          stats, sp, ties, FloorCtl{nullptr, nullptr, nullptr});
     else
 #endif
       k_sim_topk_f16<k16Cap, false, kModeEX><<<pl_re.items(), 64 * k16Waves, 0, st>>>(
           emb16, emb, nd, ex_in, ex_n, q_offset, K, cand, gkeys, ovf2, n_ovf2, nullptr, ex_seeds, kStreamMargin, 0, 1, 0,
-          nullptr, sp, ties);
+          nullptr, sp, ties, FloorCtl{nullptr, nullptr, nullptr});
   } else {
     const size_t lds = topk_lds_bytes<C>();
     static bool attr32[kMaxDev] = {false};  // a function attribute is set per device
@@ -2476,7 +2687,10 @@ int64_t fwav_tie_list_size(int64_t max_q) { return 1 + (int64_t)kTieRec * (max_q
 size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   const int64_t q = max_q > 0 ? max_q : 1;
   if (k > 64) return large_workspace_bytes(n_domains, q);
-  return f16_keys_bytes(q, n_domains) + (size_t)q * sizeof(uint32_t) + 2 * (size_t)(2 * q + 1) * sizeof(int32_t);
+  // key buffers, shared limits u32[q], two overflow lists (list, count, seeds), the floor's miss list (list, count),
+  // the floor key, the pilots' scores
+  return f16_keys_bytes(q, n_domains) + (size_t)q * sizeof(uint32_t) + 2 * (size_t)(2 * q + 1) * sizeof(int32_t) +
+         (size_t)(q + 1) * sizeof(int32_t) + sizeof(uint32_t) + (size_t)kFloorWG * kFloorPilots * kFloorJ * sizeof(float);
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,
@@ -2572,6 +2786,18 @@ int fwav_debug_topk_mode(int mode) {
 int fwav_debug_topk_geometry(int wide) {
   FWAV_CHECK_ARG(wide >= -1 && wide <= 3, FWAV_ERR_ARG, "fwav_debug_topk_geometry: outside [-1, 3]");
   g_wide = wide;
+  return FWAV_OK;
+}
+
+// Diagnostic override of the speculative floor (include/fwav_debug.h).
+int fwav_debug_topk_floor(int mode, float value) {
+  FWAV_CHECK_ARG(mode >= -1 && mode <= 2, FWAV_ERR_ARG, "fwav_debug_topk_floor: mode outside [-1, 2]");
+  FWAV_CHECK_ARG(mode != 1 || (value == value && value > -INFINITY && value < INFINITY), FWAV_ERR_ARG,
+                 "fwav_debug_topk_floor: the forced floor must be finite");
+  g_floor_mode = mode;
+  uint32_t u;
+  std::memcpy(&u, &value, sizeof u);
+  g_floor_key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // f2key
   return FWAV_OK;
 }
 

@@ -74,6 +74,7 @@ DEBUG_SIGNATURES = {
     "fwav_debug_topk_geometry": (I32, [I32]),
     "fwav_debug_topk_plan_info": (I32, [I64, I64, P, P]),
     "fwav_debug_topk_qb": (I64, [I32]),
+    "fwav_debug_topk_floor": (I32, [I32, F32]),
 }
 
 
@@ -145,7 +146,7 @@ def lib() -> C.CDLL:
 
 class debug_library:
     """``with debug_library(): ...`` routes every fwav call of the block (fwav.engine included) through
-    libfwav_debug.so, whose process-global knobs (fwav_debug_topk_plan / _mode / _geometry) the block may set; they
+    libfwav_debug.so, whose process-global knobs (fwav_debug_topk_plan / _mode / _geometry / _floor) the block may set; they
     are reset to the defaults on exit.  Test-only: not thread-safe, not re-entrant across threads."""
 
     def __enter__(self):
@@ -160,6 +161,7 @@ class debug_library:
         d.fwav_debug_topk_plan(-1, 1)
         d.fwav_debug_topk_mode(-1)
         d.fwav_debug_topk_geometry(-1)
+        d.fwav_debug_topk_floor(-1, 0.0)
         _active = self.prev
         return False
 
