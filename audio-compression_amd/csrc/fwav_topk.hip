@@ -47,8 +47,8 @@
     defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || defined(FWAV_TOPK_CVACC) || defined(FWAV_TOPK_CW) || \
     defined(FWAV_TOPK_CWPE) || defined(FWAV_TOPK_DEBUG) || defined(FWAV_TOPK_DELTA) || defined(FWAV_TOPK_EXGROW) || \
     defined(FWAV_TOPK_EXTSEED) || defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_FLOOR) || \
-    defined(FWAV_TOPK_FLOOR_MIND) || defined(FWAV_TOPK_FLOOR_MINQ) || defined(FWAV_TOPK_G) || \
-    defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
+    defined(FWAV_TOPK_FLOOR_MIND) || defined(FWAV_TOPK_FLOOR_MINQ) || defined(FWAV_TOPK_FLOOR_P2) || \
+    defined(FWAV_TOPK_G) || defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
     defined(FWAV_TOPK_INTERLEAVE) || defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_MERGE_WG) || \
     defined(FWAV_TOPK_MSKIP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
     defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SETSTATS) || \
@@ -544,7 +544,11 @@ constexpr int k16QB = 32 * k16Waves * k16Sets;  // queries per block (one workgr
 #ifndef FWAV_TOPK_MAXP
 #define FWAV_TOPK_MAXP 8
 #endif
-constexpr int kMaxPieces = FWAV_TOPK_MAXP;  // a split block's table pieces (merge: P·(C − 64) keys per query at most)
+// a first pass's table pieces per split block (merge: P·(C − 64) keys per query at most) ...
+constexpr int kPlanMaxPieces = FWAV_TOPK_MAXP;
+// ... and any plan's, the floor's second pass included (k_merge_pieces is instantiated for ≤ 8 and ≤ 16 pieces)
+constexpr int kMaxPieces = 16;
+static_assert(kPlanMaxPieces <= kMaxPieces, "first-pass plans stay within the merge's widest instantiation");
 
 // Work plan of the fp16 search.  The n_blocks query blocks are items of one launch, dispatched in order: the first
 // F = nb − R blocks stream the whole table, then each of the last R = min(nb, rt) blocks is split into P pieces of
@@ -2016,8 +2020,8 @@ __device__ __forceinline__ void merge_band(const uint64_t* __restrict__ sw, int 
   }
 }
 
-// One split-block query of k_merge_pieces (defined below the kernel).
-template <int C, int QB, bool HL>
+// One split-block query of k_merge_pieces (defined below the kernel); MP ≥ the plan's pieces.
+template <int C, int QB, bool HL, int MP>
 __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int lane, uint64_t* sw,
                                             const uint64_t* __restrict__ gkeys_all, const int32_t* __restrict__ active,
                                             int n_active, int K, int32_t* __restrict__ cand,
@@ -2026,7 +2030,7 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
                                             int64_t q_offset, const SgemvSplit& sp, int32_t* __restrict__ ties,
                                             uint32_t fkey, const FloorCtl& fl);
 
-template <int C, int QB, bool HL>
+template <int C, int QB, bool HL, int MP>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
                                                       const int32_t* __restrict__ n_active_p, int plan_rt, int plan_p,
@@ -2046,12 +2050,12 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   // profiles/r05/ab_merge_persistent.log): the merge (1.1 ms at cfg2, all 330,750 queries in 6 pieces) is bound by
   // reading the pieces' bands, not by dispatch (profiles/r05/merge_sq_cfg2.log)
   for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < plan.R * QB; w += (int64_t)gridDim.x * 4)
-    merge_query<C, QB, HL>(plan, w, lane, sw, gkeys_all, active, n_active, K, cand, ovf_list, n_ovf, share, emb,
-                           q_offset, sp, ties, fkey, fl);
+    merge_query<C, QB, HL, MP>(plan, w, lane, sw, gkeys_all, active, n_active, K, cand, ovf_list, n_ovf, share, emb,
+                               q_offset, sp, ties, fkey, fl);
 }
 
 // One split-block query w of k_merge_pieces (whole wave; sw: the wave's LDS row).
-template <int C, int QB, bool HL>
+template <int C, int QB, bool HL, int MP>
 __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int lane, uint64_t* sw,
                                             const uint64_t* __restrict__ gkeys_all, const int32_t* __restrict__ active,
                                             int n_active, int K, int32_t* __restrict__ cand,
@@ -2065,25 +2069,25 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
   const int64_t qq = slot_query(block, ql, plan.nb, QB);
   if (qq >= n_active) return;
   const int P = plan.P;
-  const uint64_t* kqs[kMaxPieces];
-  int cnt[kMaxPieces + 1];  // prefix of the pieces' band counts
+  const uint64_t* kqs[MP];
+  int cnt[MP + 1];  // prefix of the pieces' band counts
   uint32_t seed = 0u;
   cnt[0] = 0;
 #pragma unroll
-  for (int p = 0; p < kMaxPieces; ++p) {
+  for (int p = 0; p < MP; ++p) {
     const int64_t item = plan.item_of(block, p < P ? p : 0);
     kqs[p] = gkeys_all + ((size_t)item * QB + ql) * C;
     const uint64_t hdr = p < P ? kqs[p][C - 1] : 0ull;
     seed = max(seed, (uint32_t)(hdr >> 32));
     cnt[p + 1] = cnt[p] + (int)(uint32_t)hdr;
   }
-  const int n = cnt[kMaxPieces];
+  const int n = cnt[MP];
   const uint32_t Lk = share[qq];
   const int32_t qid = active[qq];
   // Load the union (entries above the shared limit) into registers, all loads issued together, take its K-th largest
   // key T by a greedy bitwise select and keep the band above T − margin (the pieces' own limits only know their local
   // K-th, which for many pieces lies far below the query's)
-  constexpr int kU = (C - 64) * kMaxPieces / 64;  // union entries per lane at most
+  constexpr int kU = (C - 64) * MP / 64;  // union entries per lane at most
   const int nu = (n + 63) >> 6;                   // registers in use (wave-uniform)
   uint64_t x[kU];
 #pragma unroll
@@ -2093,7 +2097,7 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
     const int e = u * 64 + lane;
     int p = 0;
 #pragma unroll
-    for (int pp = 1; pp < kMaxPieces; ++pp) p += e >= cnt[pp] ? 1 : 0;
+    for (int pp = 1; pp < MP; ++pp) p += e >= cnt[pp] ? 1 : 0;
     const uint64_t y = e < n ? kqs[p][e - cnt[p]] : 0ull;
     x[u] = (uint32_t)(y >> 32) > Lk ? y : 0ull;
   }
@@ -2282,7 +2286,7 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
       rt = (int)nb;
       int64_t p = slots / nb;
       if (FWAV_TOPK_PMAJOR && p < (geo == kGeoCent ? FWAV_TOPK_CPDBL : 4)) p *= 2;
-      P = (int)(p < kMaxPieces ? p : kMaxPieces);
+      P = (int)(p < kPlanMaxPieces ? p : kPlanMaxPieces);
     } else if (FWAV_TOPK_PMAJOR && 2 * nb <= 3 * slots) {
       // up to 1.5 rounds of blocks: every block in max(3, ⌊2·slots / nb⌋) pieces, piece-major — later rounds start
       // from the earlier pieces' limits (82,688 queries: 6.43 → 5.92 ms with 3 pieces; 165,375: 11.27 → 10.81 with
@@ -2296,7 +2300,7 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
       int64_t p = 2 * slots / nb;
       const int64_t pmin = (geo == kGeoCent) ? FWAV_TOPK_CPMIN : 3;
       if (p < pmin) p = pmin;
-      P = (int)(p < kMaxPieces ? p : kMaxPieces);
+      P = (int)(p < kPlanMaxPieces ? p : kPlanMaxPieces);
     } else {
       const int64_t last = nb % slots == 0 ? slots : nb % slots;  // blocks in the last round
       if (last > cus) {
@@ -2335,23 +2339,35 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
 #ifndef FWAV_TOPK_FLOOR_MIND
 #define FWAV_TOPK_FLOOR_MIND 65536
 #endif
+#ifndef FWAV_TOPK_FLOOR_P2
+#define FWAV_TOPK_FLOOR_P2 16  // the second pass's table pieces per split block
+#endif
 constexpr int kFloorPilots = 512;  // pilot queries (evenly spaced over the active list), one k_floor_reduce thread each
 constexpr int kFloorWG = 256;      // k_floor_pilot workgroups, each over a 1/kFloorWG slice of the sampled domains
-constexpr int kFloorJ = 4;         // the pilot's estimate: its j-th best score over every (K/j)-th domain ≈ its K-th
-constexpr int kFloorSplit = 32;    // second pass: blocks split into kMaxPieces table pieces (the rest whole-table)
+constexpr int kFloorJ = 8;         // the pilot's estimate: its j-th best score over every (K/j)-th domain ≈ its K-th
+#ifndef FWAV_TOPK_FLOOR_RANK
+#define FWAV_TOPK_FLOOR_RANK 5     // the floor: the pilots' RANK-th smallest estimate (≈ their 1 % quantile)
+#endif
+// second pass: up to kFloorSplit blocks (of 256 misses) split into FWAV_TOPK_FLOOR_P2 pieces, any further ones
+// whole-table (a floor that cut more than 5 % of cfg2's queries)
+constexpr int kFloorSplit = 64;
+static_assert(FWAV_TOPK_FLOOR_P2 >= 1 && FWAV_TOPK_FLOOR_P2 <= kMaxPieces, "second-pass pieces outside the merge");
 #ifdef FWAV_DEBUG_API
 static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 forced value, 2 pilot at any size
 static uint32_t g_floor_key = 0u;
+static int g_floor_rank = FWAV_TOPK_FLOOR_RANK;
 #else
 constexpr int g_floor_mode = -1;
 constexpr uint32_t g_floor_key = 0u;
+constexpr int g_floor_rank = FWAV_TOPK_FLOOR_RANK;
 #endif
 static int floor_mode() { return FWAV_TOPK_FLOOR ? g_floor_mode : 0; }
-// second-pass plan (base geometry) for a miss list of at most max_q queries
-static void floor_plan(int64_t max_q, int& rt, int& P) {
+// second-pass plan (base geometry) for a miss list of at most max_q queries: every piece streams ≥ 16 chunks
+static void floor_plan(int64_t max_q, int64_t nd, int& rt, int& P) {
   (void)max_q;
   rt = kFloorSplit;
-  P = kMaxPieces;
+  const int64_t pmax = cdiv(nd, kChunk) / 16;
+  P = (int)std::max<int64_t>(1, std::min<int64_t>(FWAV_TOPK_FLOOR_P2, pmax));
 }
 
 // Each pilot p (of kFloorPilots, 2 per thread) at active position p·n/kFloorPilots: its kFloorJ best f32 scores over
@@ -2416,12 +2432,12 @@ __global__ __launch_bounds__(256) void k_floor_pilot(const float* __restrict__ e
       scratch[((int64_t)blockIdx.x * kFloorPilots + threadIdx.x * 2 + i) * kFloorJ + k] = top[i][k];
 }
 
-// Thread p: pilot p's j-th best over all slices (its estimate of its K-th score); the floor is the smallest estimate
-// (key in f2key order; 0 = no floor: fewer than min_q active queries, or no finite estimate).
+// Thread p: pilot p's j-th best over all slices (its estimate of its K-th score); the floor is the rank-th smallest
+// estimate (key in f2key order; 0 = no floor: fewer than min_q active queries, or no finite estimate).
 __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __restrict__ scratch, int nwg, int j,
-                                                               const int32_t* __restrict__ n_active_p, int min_q,
-                                                               uint32_t* __restrict__ floor_key) {
-  __shared__ float red[kFloorPilots / 64];
+                                                               int rank, const int32_t* __restrict__ n_active_p,
+                                                               int min_q, uint32_t* __restrict__ floor_key) {
+  __shared__ float est[kFloorPilots];
   const int p = threadIdx.x;
   float top[kFloorJ];
 #pragma unroll
@@ -2441,12 +2457,20 @@ __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __re
   float e = top[0];
 #pragma unroll
   for (int k = 1; k < kFloorJ; ++k) e = k == j - 1 ? top[k] : e;
-  for (int off = 32; off > 0; off >>= 1) e = fminf(e, __shfl_xor(e, off));
-  if ((p & 63) == 0) red[p >> 6] = e;
+  est[p] = e;
   __syncthreads();
   if (p == 0) {
-    float m = red[0];
-    for (int w = 1; w < kFloorPilots / 64; ++w) m = fminf(m, red[w]);
+    // rank-th smallest: rank passes of "smallest above the previous one" (ties counted with their multiplicity)
+    float m = -INFINITY;
+    int below = 0;
+    while (below < rank) {
+      float nxt = INFINITY;
+      int c = 0;
+      for (int i = 0; i < kFloorPilots; ++i) nxt = fminf(nxt, est[i] > m ? est[i] : INFINITY);
+      for (int i = 0; i < kFloorPilots; ++i) c += est[i] == nxt ? 1 : 0;
+      m = nxt;
+      below += c > 0 ? c : rank;  // (no larger estimate left: stop at the largest)
+    }
     const int na = *n_active_p;
     floor_key[0] = (na >= min_q && na > 0 && m > -INFINITY && m < INFINITY) ? f2key(m) : 0u;
   }
@@ -2459,7 +2483,7 @@ static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
   size_t items_q = (size_t)make_plan(q, 0, 1, k16QB).items() * k16QB;
   {
     int rt2, P2;
-    floor_plan(q, rt2, P2);
+    floor_plan(q, nd, rt2, P2);
     const size_t n2 = (size_t)make_plan(q, rt2, P2, k16QB).items() * k16QB;
     items_q = n2 > items_q ? n2 : items_q;
   }
@@ -2583,9 +2607,13 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
         int cus, per_cu;
         topk_device_slots(g, cus, per_cu);
         const int64_t mgrid_cap = (int64_t)cus * FWAV_TOPK_MERGE_WG;
-#define FWAV_MERGE(QB_, HL_)                                                                                    \
-  k_merge_pieces<k16Cap, QB_, HL_><<<std::min<int64_t>(cdiv(pl.R * QB_, 4), mgrid_cap), 256, 0, st>>>(          \
+#define FWAV_MERGE_MP(QB_, HL_, MP_)                                                                            \
+  k_merge_pieces<k16Cap, QB_, HL_, MP_><<<std::min<int64_t>(cdiv(pl.R * QB_, 4), mgrid_cap), 256, 0, st>>>(     \
       gkeys, act, nact, rt, P, K, cand, ovf1, n_ovf1, share, emb, q_offset, sp, ties, fl)
+#define FWAV_MERGE(QB_, HL_)                                                                                    \
+  do {                                                                                                          \
+    if (pl.P <= 8) FWAV_MERGE_MP(QB_, HL_, 8); else FWAV_MERGE_MP(QB_, HL_, kMaxPieces);                        \
+  } while (0)
         if (g == kGeoWide) {
           if (mode1 == kModeHL) FWAV_MERGE(kWideQB, true); else FWAV_MERGE(kWideQB, false);
         } else if (g == kGeoCent) {
@@ -2596,6 +2624,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
           if (mode1 == kModeHL) FWAV_MERGE(k16QB, true); else FWAV_MERGE(k16QB, false);
         }
 #undef FWAV_MERGE
+#undef FWAV_MERGE_MP
       }
     };
     int rt, P;
@@ -2614,14 +2643,15 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       } else {
         const int j = K < kFloorJ ? K : kFloorJ, stride = K / j;
         k_floor_pilot<<<kFloorWG, 256, 0, st>>>(emb, nd, active, n_active, q_offset, stride, pilot);
-        k_floor_reduce<<<1, kFloorPilots, 0, st>>>(pilot, kFloorWG, j, n_active, FWAV_TOPK_FLOOR_MINQ, floor_key);
+        k_floor_reduce<<<1, kFloorPilots, 0, st>>>(pilot, kFloorWG, j, g_floor_rank, n_active,
+                                                   fmode == 2 ? 0 : FWAV_TOPK_FLOOR_MINQ, floor_key);
       }
       fl = FloorCtl{floor_key, miss, n_miss};
     }
     first_pass(active, n_active, geo, rt, P, fl, true);
     if (use_floor) {
       int rt2, P2;
-      floor_plan(max_q, rt2, P2);
+      floor_plan(max_q, nd, rt2, P2);
       first_pass(miss, n_miss, kGeoBase, rt2, P2, FloorCtl{nullptr, nullptr, nullptr}, false);
     }
     // Queries whose band overflowed the buffer (large groups of equal or nearly equal scores) are searched again by
@@ -2795,6 +2825,7 @@ int fwav_debug_topk_floor(int mode, float value) {
   FWAV_CHECK_ARG(mode != 1 || (value == value && value > -INFINITY && value < INFINITY), FWAV_ERR_ARG,
                  "fwav_debug_topk_floor: the forced floor must be finite");
   g_floor_mode = mode;
+  g_floor_rank = mode == 2 && value >= 1.0f && value <= (float)kFloorPilots ? (int)value : FWAV_TOPK_FLOOR_RANK;
   uint32_t u;
   std::memcpy(&u, &value, sizeof u);
   g_floor_key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // f2key
@@ -2807,7 +2838,7 @@ int fwav_debug_topk_floor(int mode, float value) {
 // times.  *items = the launch's grid.
 int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t* count, int64_t* items) {
   FWAV_CHECK_ARG(n >= 0 && count && items && wide >= 0 && wide <= 3 &&
-                     (pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces)), FWAV_ERR_ARG,
+                     (pieces == -1 || (pieces >= 1 && pieces <= kPlanMaxPieces)), FWAV_ERR_ARG,
                  "fwav_debug_topk_plan_cover: bad args");
   const int geo = wide;  // 0 base, 1 wide, 2 centroid, 3 centroid wide
   const int W = (geo == kGeoWide || geo == kGeoCentWide) ? kWideW : (geo == kGeoCent ? kCentW : k16Waves);
@@ -2853,7 +2884,7 @@ int64_t fwav_debug_topk_qb(int geo) { return geo >= 0 && geo <= 3 ? geometry_qb(
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.
 int fwav_debug_topk_plan(int rt, int pieces) {
-  FWAV_CHECK_ARG(pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces), FWAV_ERR_ARG,
+  FWAV_CHECK_ARG(pieces == -1 || (pieces >= 1 && pieces <= kPlanMaxPieces), FWAV_ERR_ARG,
                  "fwav_debug_topk_plan: pieces outside [1, 8] (or -1: query halves)");
   g_plan_rt = rt;
   g_plan_p = rt < 0 ? -1 : pieces;

@@ -28,18 +28,20 @@ nd, nr = r.n_domains, r.n_ranges
 st = torch.cuda.current_stream().cuda_stream
 emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 call("fwav_emb16_from_emb", r.emb.data_ptr(), nd, emb16.data_ptr(), st)
-TAIL = 4 + 4 * 256 * 512 * 4  # after the miss list's count: the floor key, the pilots' scores
+TAIL = 4 + 4 * 256 * 512 * 8  # after the miss list's count: the floor key, the pilots' scores
+CONFIGS = [(0, 0.0), (-1, 0.0), (2, 1.0), (2, 3.0), (2, 10.0), (2, 20.0)]  # (mode, value): off, default, ranks
 for nq in (nr, 41344):
     active = torch.arange(nq, dtype=torch.int32, device="cuda")
     n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
     wsn = size_call("fwav_sim_topk_workspace_size", nq, nd, 64)
     wsk = torch.zeros(wsn, dtype=torch.uint8, device="cuda")
-    times = {0: [], -1: []}
-    cands = {}
-    info = ""
+    times = {c: [] for c in CONFIGS}
+    info = {}
+    ref = None
+    same = True
     for rep in range(reps + 1):
-        for mode in (0, -1):
-            call("fwav_debug_topk_floor", mode, 0.0)
+        for c in CONFIGS:
+            call("fwav_debug_topk_floor", c[0], c[1])
             cand = torch.empty(nr * 64, dtype=torch.int32, device="cuda")
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -48,14 +50,18 @@ for nq in (nr, 41344):
             e1.record()
             torch.cuda.synchronize()
             if rep:
-                times[mode].append(e0.elapsed_time(e1))
-            cands[mode] = cand[:nq * 64].clone()
-            if mode == -1:
+                times[c].append(e0.elapsed_time(e1))
+            if ref is None:
+                ref = cand[:nq * 64].clone()
+            same = same and bool(torch.equal(cand[:nq * 64], ref))
+            if c[0] != 0:
                 tail = wsk[wsn - TAIL - 4:wsn - TAIL + 4].cpu().numpy().tobytes()
                 n_miss, key = struct.unpack("<iI", tail)
                 u = (key & 0x7FFFFFFF) if key & 0x80000000 else (~key & 0xFFFFFFFF)
                 fl = struct.unpack("<f", struct.pack("<I", u))[0] if key else float("nan")
-                info = f"floor {fl:.4f}, {n_miss} queries in the second pass"
+                info[c] = f"floor {fl:.4f}, {n_miss} in the second pass"
     call("fwav_debug_topk_floor", -1, 0.0)
-    print(f"{nq} queries: floor off median {np.median(times[0]):.3f} ms, floor on {np.median(times[-1]):.3f} ms "
-          f"({info}); identical={bool(torch.equal(cands[0], cands[-1]))}", flush=True)
+    for c in CONFIGS:
+        name = {0: "off", -1: "default"}.get(c[0], f"rank {int(c[1])}")
+        print(f"{nq} queries, floor {name}: median {np.median(times[c]):.3f} ms  {info.get(c, '')}", flush=True)
+    print(f"{nq} queries: all candidates identical={same}", flush=True)
