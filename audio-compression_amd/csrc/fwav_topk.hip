@@ -2333,8 +2333,11 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
 #ifndef FWAV_TOPK_FLOOR
 #define FWAV_TOPK_FLOOR 1
 #endif
+// The second pass costs one round of cold table pieces (≈ 1.5 ms whatever its size: a piece's cost is the rise of its
+// limit from nothing), so the floor pays only where it saves more than that: cfg2 (330,750 queries) 18.02 → 16.82 ms,
+// but one rank's share at N = 8 (41,344) 3.46 → 4.45 ms (tools/floor_pass_ab.py, profiles/r05/floor_pass_ab.log)
 #ifndef FWAV_TOPK_FLOOR_MINQ
-#define FWAV_TOPK_FLOOR_MINQ 32768
+#define FWAV_TOPK_FLOOR_MINQ 262144
 #endif
 #ifndef FWAV_TOPK_FLOOR_MIND
 #define FWAV_TOPK_FLOOR_MIND 65536
@@ -2351,9 +2354,14 @@ constexpr int kFloorJ = 8;         // the pilot's estimate: its j-th best score 
 // second pass: up to kFloorSplit blocks (of 256 misses) split into FWAV_TOPK_FLOOR_P2 pieces, any further ones
 // whole-table (a floor that cut more than 5 % of cfg2's queries)
 constexpr int kFloorSplit = 64;
+// The second pass runs at a lower floor, the pilots' smallest estimate − kFloor2Margin (below every K-th score of cfg2:
+// the smallest of all 330,750 is 1.720, the pilots' smallest estimate ≈ 1.75), so that its table pieces do not start
+// cold either; the queries that one cuts (normally none) take a floor-free third pass.  (Full score rows for them,
+// launch_topk_large, measured 3.6 ms per launch: one workgroup per row streams it several times.)
+constexpr float kFloor2Margin = 0.06f;
 static_assert(FWAV_TOPK_FLOOR_P2 >= 1 && FWAV_TOPK_FLOOR_P2 <= kMaxPieces, "second-pass pieces outside the merge");
 #ifdef FWAV_DEBUG_API
-static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 forced value, 2 pilot at any size
+static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 / 3 forced value, 2 pilot at any size
 static uint32_t g_floor_key = 0u;
 static int g_floor_rank = FWAV_TOPK_FLOOR_RANK;
 #else
@@ -2415,12 +2423,14 @@ __global__ __launch_bounds__(256) void k_floor_pilot(const float* __restrict__ e
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           x += q[i][4 * k] * d[k].x + q[i][4 * k + 1] * d[k].y + q[i][4 * k + 2] * d[k].z + q[i][4 * k + 3] * d[k].w;
-        // sorted insertion into the pilot's top kFloorJ (descending)
+        // sorted insertion into the pilot's top kFloorJ (descending), only for a score that enters it
+        if (x > top[i][kFloorJ - 1]) {
 #pragma unroll
-        for (int k = 0; k < kFloorJ; ++k) {
-          const float hi = fmaxf(top[i][k], x);
-          x = fminf(top[i][k], x);
-          top[i][k] = hi;
+          for (int k = 0; k < kFloorJ; ++k) {
+            const float hi = fmaxf(top[i][k], x);
+            x = fminf(top[i][k], x);
+            top[i][k] = hi;
+          }
         }
       }
     }
@@ -2437,6 +2447,7 @@ __global__ __launch_bounds__(256) void k_floor_pilot(const float* __restrict__ e
 __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __restrict__ scratch, int nwg, int j,
                                                                int rank, const int32_t* __restrict__ n_active_p,
                                                                int min_q, uint32_t* __restrict__ floor_key) {
+  // floor_key[0]: the first pass's floor; floor_key[1]: the second pass's, the smallest estimate − kFloor2Margin
   __shared__ float est[kFloorPilots];
   const int p = threadIdx.x;
   float top[kFloorJ];
@@ -2446,11 +2457,13 @@ __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __re
 #pragma unroll
     for (int i = 0; i < kFloorJ; ++i) {
       float x = scratch[((int64_t)b * kFloorPilots + p) * kFloorJ + i];
+      if (x > top[kFloorJ - 1]) {
 #pragma unroll
-      for (int k = 0; k < kFloorJ; ++k) {
-        const float hi = fmaxf(top[k], x);
-        x = fminf(top[k], x);
-        top[k] = hi;
+        for (int k = 0; k < kFloorJ; ++k) {
+          const float hi = fmaxf(top[k], x);
+          x = fminf(top[k], x);
+          top[k] = hi;
+        }
       }
     }
   }
@@ -2459,21 +2472,17 @@ __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __re
   for (int k = 1; k < kFloorJ; ++k) e = k == j - 1 ? top[k] : e;
   est[p] = e;
   __syncthreads();
-  if (p == 0) {
-    // rank-th smallest: rank passes of "smallest above the previous one" (ties counted with their multiplicity)
-    float m = -INFINITY;
-    int below = 0;
-    while (below < rank) {
-      float nxt = INFINITY;
-      int c = 0;
-      for (int i = 0; i < kFloorPilots; ++i) nxt = fminf(nxt, est[i] > m ? est[i] : INFINITY);
-      for (int i = 0; i < kFloorPilots; ++i) c += est[i] == nxt ? 1 : 0;
-      m = nxt;
-      below += c > 0 ? c : rank;  // (no larger estimate left: stop at the largest)
-    }
-    const int na = *n_active_p;
-    floor_key[0] = (na >= min_q && na > 0 && m > -INFINITY && m < INFINITY) ? f2key(m) : 0u;
+  // every pilot's place in (estimate, pilot) order: the one at place rank − 1 is the floor, the one at place 0 the
+  // second pass's floor (+ kFloor2Margin)
+  int place = 0;
+  for (int i = 0; i < kFloorPilots; ++i) {
+    const float x = est[i];
+    place += (x < e || (x == e && i < p)) ? 1 : 0;
   }
+  const int na = *n_active_p;
+  const bool ok = na >= min_q && na > 0 && e > -INFINITY && e < INFINITY;
+  if (place == rank - 1) floor_key[0] = ok ? f2key(e) : 0u;
+  if (place == 0) floor_key[1] = ok ? f2key(e - kFloor2Margin) : 0u;
 }
 
 // Key-buffer bytes: enough for the first pass in either geometry (a diagnostic override may switch it between the
@@ -2540,10 +2549,13 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     const int geo = stats_first && !(dbg & (1 << 18)) ? kGeoBase : first_geometry(nd, max_q);
     const int mode1 = first_mode(nd);
     // workspace after the two overflow lists: the floor's miss list (list[q], count), the floor key, the pilot scores
+    // (miss list + count of the first and of the second pass, two floor keys, the score-row / last-pass counts)
     int32_t* miss = const_cast<int32_t*>(reinterpret_cast<const int32_t*>(seeds1 + q1));
     int32_t* n_miss = miss + q1;
-    uint32_t* floor_key = reinterpret_cast<uint32_t*>(n_miss + 1);
-    float* pilot = reinterpret_cast<float*>(floor_key + 1);
+    int32_t* miss2 = n_miss + 1;
+    int32_t* n_miss2 = miss2 + q1;
+    uint32_t* floor_key = reinterpret_cast<uint32_t*>(n_miss2 + 1);
+    float* pilot = reinterpret_cast<float*>(floor_key + 2);
     // One first pass (search + merge of split blocks) over act[0 .. *nact) in geometry g with plan (rt, P) and floor
     // fl; `diag`: the debug library's counter / ablation launches may replace the search
     auto first_pass = [&](const int32_t* act, const int32_t* nact, int g, int rt, int P, FloorCtl fl, bool diag) {
@@ -2638,8 +2650,10 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     FloorCtl fl{nullptr, nullptr, nullptr};
     if (use_floor) {
       (void)hipMemsetAsync(n_miss, 0, sizeof(int32_t), st);
-      if (fmode == 1) {  // debug: a forced floor value
+      (void)hipMemsetAsync(n_miss2, 0, sizeof(int32_t), st);
+      if (fmode == 1 || fmode == 3) {  // debug: a forced floor value (3: the second pass's too)
         (void)hipMemsetD32Async((hipDeviceptr_t)floor_key, (int)g_floor_key, 1, st);
+        (void)hipMemsetD32Async((hipDeviceptr_t)(floor_key + 1), fmode == 3 ? (int)g_floor_key : 0, 1, st);
       } else {
         const int j = K < kFloorJ ? K : kFloorJ, stride = K / j;
         k_floor_pilot<<<kFloorWG, 256, 0, st>>>(emb, nd, active, n_active, q_offset, stride, pilot);
@@ -2652,7 +2666,8 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     if (use_floor) {
       int rt2, P2;
       floor_plan(max_q, nd, rt2, P2);
-      first_pass(miss, n_miss, kGeoBase, rt2, P2, FloorCtl{nullptr, nullptr, nullptr}, false);
+      first_pass(miss, n_miss, kGeoBase, rt2, P2, FloorCtl{floor_key + 1, miss2, n_miss2}, false);
+      first_pass(miss2, n_miss2, kGeoBase, rt2, P2, FloorCtl{nullptr, nullptr, nullptr}, false);
     }
     // Queries whose band overflowed the buffer (large groups of equal or nearly equal scores) are searched again by
     // the same kernel in a narrower mode, on the device-side overflow list (no host sync; a relaunch exits at once
@@ -2717,10 +2732,11 @@ int64_t fwav_tie_list_size(int64_t max_q) { return 1 + (int64_t)kTieRec * (max_q
 size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   const int64_t q = max_q > 0 ? max_q : 1;
   if (k > 64) return large_workspace_bytes(n_domains, q);
-  // key buffers, shared limits u32[q], two overflow lists (list, count, seeds), the floor's miss list (list, count),
-  // the floor key, the pilots' scores
+  // key buffers, shared limits u32[q], two overflow lists (list, count, seeds), the floor's two miss lists (list,
+  // count), its two keys, the pilots' scores
   return f16_keys_bytes(q, n_domains) + (size_t)q * sizeof(uint32_t) + 2 * (size_t)(2 * q + 1) * sizeof(int32_t) +
-         (size_t)(q + 1) * sizeof(int32_t) + sizeof(uint32_t) + (size_t)kFloorWG * kFloorPilots * kFloorJ * sizeof(float);
+         2 * (size_t)(q + 1) * sizeof(int32_t) + 2 * sizeof(uint32_t) +
+         (size_t)kFloorWG * kFloorPilots * kFloorJ * sizeof(float);
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,
@@ -2821,8 +2837,8 @@ int fwav_debug_topk_geometry(int wide) {
 
 // Diagnostic override of the speculative floor (include/fwav_debug.h).
 int fwav_debug_topk_floor(int mode, float value) {
-  FWAV_CHECK_ARG(mode >= -1 && mode <= 2, FWAV_ERR_ARG, "fwav_debug_topk_floor: mode outside [-1, 2]");
-  FWAV_CHECK_ARG(mode != 1 || (value == value && value > -INFINITY && value < INFINITY), FWAV_ERR_ARG,
+  FWAV_CHECK_ARG(mode >= -1 && mode <= 3, FWAV_ERR_ARG, "fwav_debug_topk_floor: mode outside [-1, 3]");
+  FWAV_CHECK_ARG((mode != 1 && mode != 3) || (value == value && value > -INFINITY && value < INFINITY), FWAV_ERR_ARG,
                  "fwav_debug_topk_floor: the forced floor must be finite");
   g_floor_mode = mode;
   g_floor_rank = mode == 2 && value >= 1.0f && value <= (float)kFloorPilots ? (int)value : FWAV_TOPK_FLOOR_RANK;

@@ -1,7 +1,8 @@
 """The fp16 search's speculative floor (fwav_topk.hip, FloorCtl): a first pass whose band limits start at a floor
 guessed from pilot queries, the queries it may have cut searched again without it.  Whatever the floor, the candidates
 and every match tuple must equal the all-f32 search's: a floor below every score (nothing cut), floors inside the
-range of the K-th scores (some queries cut), one above every score (every query cut), and the pilots' own floor — under
+range of the K-th scores (some queries cut), one above every score (every query cut), and the pilots' own floor; the
+same floor for the second pass too, so that its cuts take the floor-free third pass — under
 each first-pass mode and geometry, with split plans, and on a signal whose bands overflow."""
 import numpy as np
 import pytest
@@ -64,7 +65,9 @@ def test_floor_any_value_equals_f32(gen):
     kth = _kth_scores(ref[1], ref[0])
     assert len(kth) > 1000
     qs = [float(np.quantile(kth, p)) for p in (0.01, 0.3, 0.7)]
-    floors = [(0, 0.0), (1, -10.0), *[(1, v) for v in qs], (1, float(kth.max()) + 0.01), (1, 10.0), (2, 0.0)]
+    # mode 3: the second pass at the same floor, so the queries it cuts go on to the floor-free third pass
+    floors = [(0, 0.0), (1, -10.0), *[(1, v) for v in qs], (1, float(kth.max()) + 0.01), (1, 10.0), (2, 0.0),
+              (3, qs[0]), (3, qs[1]), (3, 10.0)]
     _check(sig, tile, K, floors, ref)
 
 
@@ -85,7 +88,7 @@ def test_floor_every_geometry(geometry):
     sig = mk()
     b, rb = _run(sig, tile, K, "f32")
     kth = _kth_scores(rb, b)
-    for mode, value in ((1, float(np.median(kth))), (2, 0.0)):
+    for mode, value in ((1, float(np.median(kth))), (2, 0.0), (3, float(np.quantile(kth, 0.05)))):
         call("fwav_debug_topk_floor", mode, value)
         a, _ = _run(sig, tile, K, "f16")
         assert np.array_equal(a, b), (geometry, mode, value)

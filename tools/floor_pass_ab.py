@@ -28,7 +28,7 @@ nd, nr = r.n_domains, r.n_ranges
 st = torch.cuda.current_stream().cuda_stream
 emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 call("fwav_emb16_from_emb", r.emb.data_ptr(), nd, emb16.data_ptr(), st)
-TAIL = 4 + 4 * 256 * 512 * 8  # after the miss list's count: the floor key, the pilots' scores
+TAIL = 4 * 256 * 512 * 8 + 8  # after the second miss list's count: two floor keys, the pilots' scores
 CONFIGS = [(0, 0.0), (-1, 0.0), (2, 1.0), (2, 3.0), (2, 10.0), (2, 20.0)]  # (mode, value): off, default, ranks
 for nq in (nr, 41344):
     active = torch.arange(nq, dtype=torch.int32, device="cuda")
@@ -55,11 +55,12 @@ for nq in (nr, 41344):
                 ref = cand[:nq * 64].clone()
             same = same and bool(torch.equal(cand[:nq * 64], ref))
             if c[0] != 0:
-                tail = wsk[wsn - TAIL - 4:wsn - TAIL + 4].cpu().numpy().tobytes()
-                n_miss, key = struct.unpack("<iI", tail)
+                b = wsk[wsn - TAIL - 4 * (nq + 1) - 4:wsn - TAIL + 4].cpu().numpy().tobytes()
+                n_miss = struct.unpack("<i", b[:4])[0]
+                n_miss2, key = struct.unpack("<iI", b[-8:])
                 u = (key & 0x7FFFFFFF) if key & 0x80000000 else (~key & 0xFFFFFFFF)
                 fl = struct.unpack("<f", struct.pack("<I", u))[0] if key else float("nan")
-                info[c] = f"floor {fl:.4f}, {n_miss} in the second pass"
+                info[c] = f"floor {fl:.4f}, {n_miss} in the second pass, {n_miss2} after it"
     call("fwav_debug_topk_floor", -1, 0.0)
     for c in CONFIGS:
         name = {0: "off", -1: "default"}.get(c[0], f"rank {int(c[1])}")
