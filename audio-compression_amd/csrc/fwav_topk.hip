@@ -2345,8 +2345,8 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
 #ifndef FWAV_TOPK_FLOOR_P2
 #define FWAV_TOPK_FLOOR_P2 16  // the second pass's table pieces per split block
 #endif
-constexpr int kFloorPilots = 512;  // pilot queries (evenly spaced over the active list), one k_floor_reduce thread each
-constexpr int kFloorWG = 256;      // k_floor_pilot workgroups, each over a 1/kFloorWG slice of the sampled domains
+constexpr int kFloorPilots = 512;  // pilot queries (evenly spaced over the active list)
+constexpr int kFloorWG = 1024;     // k_floor_pilot workgroups, each over a 1/kFloorWG slice of the sampled domains
 constexpr int kFloorJ = 8;         // the pilot's estimate: its j-th best score over every (K/j)-th domain ≈ its K-th
 #ifndef FWAV_TOPK_FLOOR_RANK
 #define FWAV_TOPK_FLOOR_RANK 5     // the floor: the pilots' RANK-th smallest estimate (≈ their 1 % quantile)
@@ -2379,8 +2379,8 @@ static void floor_plan(int64_t max_q, int64_t nd, int& rt, int& P) {
 }
 
 // Each pilot p (of kFloorPilots, 2 per thread) at active position p·n/kFloorPilots: its kFloorJ best f32 scores over
-// the sampled domains m·stride of this workgroup's slice, to scratch[(block·kFloorPilots + p)·kFloorJ + i].  The
-// slice's domain rows are staged in LDS 256 at a time.  (A guess only: no reference order needed.)
+// the sampled domains m·stride of this workgroup's slice, to scratch[(p·gridDim + block)·kFloorJ + i].  The slice's
+// domain rows are staged in LDS 256 at a time.  (A guess only: no reference order needed.)
 __global__ __launch_bounds__(256) void k_floor_pilot(const float* __restrict__ emb, int64_t nd,
                                                      const int32_t* __restrict__ active,
                                                      const int32_t* __restrict__ n_active_p, int64_t q_offset,
@@ -2419,10 +2419,15 @@ __global__ __launch_bounds__(256) void k_floor_pilot(const float* __restrict__ e
       for (int k = 0; k < 4; ++k) d[k] = rows[r][k];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        float x = 0.0f;
+        // two independent partial sums (a shorter dependent chain)
+        float x0 = 0.0f, x1 = 0.0f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          x += q[i][4 * k] * d[k].x + q[i][4 * k + 1] * d[k].y + q[i][4 * k + 2] * d[k].z + q[i][4 * k + 3] * d[k].w;
+        for (int k = 0; k < 2; ++k) {
+          x0 += q[i][4 * k] * d[k].x + q[i][4 * k + 1] * d[k].y + q[i][4 * k + 2] * d[k].z + q[i][4 * k + 3] * d[k].w;
+          x1 += q[i][8 + 4 * k] * d[2 + k].x + q[i][9 + 4 * k] * d[2 + k].y + q[i][10 + 4 * k] * d[2 + k].z +
+                q[i][11 + 4 * k] * d[2 + k].w;
+        }
+        float x = x0 + x1;
         // sorted insertion into the pilot's top kFloorJ (descending), only for a score that enters it
         if (x > top[i][kFloorJ - 1]) {
 #pragma unroll
@@ -2439,37 +2444,53 @@ __global__ __launch_bounds__(256) void k_floor_pilot(const float* __restrict__ e
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int k = 0; k < kFloorJ; ++k)
-      scratch[((int64_t)blockIdx.x * kFloorPilots + threadIdx.x * 2 + i) * kFloorJ + k] = top[i][k];
+      scratch[((int64_t)(threadIdx.x * 2 + i) * gridDim.x + blockIdx.x) * kFloorJ + k] = top[i][k];
 }
 
-// Thread p: pilot p's j-th best over all slices (its estimate of its K-th score); the floor is the rank-th smallest
-// estimate (key in f2key order; 0 = no floor: fewer than min_q active queries, or no finite estimate).
-__global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __restrict__ scratch, int nwg, int j,
-                                                               int rank, const int32_t* __restrict__ n_active_p,
-                                                               int min_q, uint32_t* __restrict__ floor_key) {
-  // floor_key[0]: the first pass's floor; floor_key[1]: the second pass's, the smallest estimate − kFloor2Margin
-  __shared__ float est[kFloorPilots];
-  const int p = threadIdx.x;
+// One wave per pilot (block = pilot): its j-th best score over all nwg slices (its estimate of its K-th score), to
+// est[pilot].  Each lane keeps the top kFloorJ of its slices' entries; then kFloorJ rounds take the wave's largest
+// head (the lowest lane holding it pops it).
+__global__ __launch_bounds__(64) void k_floor_est(const float* __restrict__ scratch, int nwg, int j,
+                                                  float* __restrict__ est) {
+  const int lane = threadIdx.x;
+  const float* sp = scratch + (int64_t)blockIdx.x * nwg * kFloorJ;
   float top[kFloorJ];
 #pragma unroll
   for (int k = 0; k < kFloorJ; ++k) top[k] = -INFINITY;
-  for (int b = 0; b < nwg; ++b) {
+  for (int e = lane; e < nwg * kFloorJ; e += 64) {
+    float x = sp[e];
+    if (x > top[kFloorJ - 1]) {
 #pragma unroll
-    for (int i = 0; i < kFloorJ; ++i) {
-      float x = scratch[((int64_t)b * kFloorPilots + p) * kFloorJ + i];
-      if (x > top[kFloorJ - 1]) {
-#pragma unroll
-        for (int k = 0; k < kFloorJ; ++k) {
-          const float hi = fmaxf(top[k], x);
-          x = fminf(top[k], x);
-          top[k] = hi;
-        }
+      for (int k = 0; k < kFloorJ; ++k) {
+        const float hi = fmaxf(top[k], x);
+        x = fminf(top[k], x);
+        top[k] = hi;
       }
     }
   }
-  float e = top[0];
+  float got = -INFINITY;
+  for (int r = 0; r < j; ++r) {
+    float m = top[0];
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    const uint64_t who = __ballot(top[0] == m);
+    if (lane == __builtin_ctzll(who)) {
 #pragma unroll
-  for (int k = 1; k < kFloorJ; ++k) e = k == j - 1 ? top[k] : e;
+      for (int k = 0; k + 1 < kFloorJ; ++k) top[k] = top[k + 1];
+      top[kFloorJ - 1] = -INFINITY;
+    }
+    got = m;
+  }
+  if (lane == 0) est[blockIdx.x] = got;
+}
+
+// The floors from the pilots' estimates: the rank-th smallest (key in f2key order; 0 = no floor: fewer than min_q
+// active queries, or no finite estimate) and the smallest − kFloor2Margin for the second pass.
+__global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __restrict__ est_g, int rank,
+                                                               const int32_t* __restrict__ n_active_p, int min_q,
+                                                               uint32_t* __restrict__ floor_key) {
+  __shared__ float est[kFloorPilots];
+  const int p = threadIdx.x;
+  const float e = est_g[p];
   est[p] = e;
   __syncthreads();
   // every pilot's place in (estimate, pilot) order: the one at place rank − 1 is the floor, the one at place 0 the
@@ -2656,9 +2677,11 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
         (void)hipMemsetD32Async((hipDeviceptr_t)(floor_key + 1), fmode == 3 ? (int)g_floor_key : 0, 1, st);
       } else {
         const int j = K < kFloorJ ? K : kFloorJ, stride = K / j;
+        float* est = pilot + (size_t)kFloorWG * kFloorPilots * kFloorJ;
         k_floor_pilot<<<kFloorWG, 256, 0, st>>>(emb, nd, active, n_active, q_offset, stride, pilot);
-        k_floor_reduce<<<1, kFloorPilots, 0, st>>>(pilot, kFloorWG, j, g_floor_rank, n_active,
-                                                   fmode == 2 ? 0 : FWAV_TOPK_FLOOR_MINQ, floor_key);
+        k_floor_est<<<kFloorPilots, 64, 0, st>>>(pilot, kFloorWG, j, est);
+        k_floor_reduce<<<1, kFloorPilots, 0, st>>>(est, g_floor_rank, n_active, fmode == 2 ? 0 : FWAV_TOPK_FLOOR_MINQ,
+                                                   floor_key);
       }
       fl = FloorCtl{floor_key, miss, n_miss};
     }
@@ -2736,7 +2759,7 @@ size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   // count), its two keys, the pilots' scores
   return f16_keys_bytes(q, n_domains) + (size_t)q * sizeof(uint32_t) + 2 * (size_t)(2 * q + 1) * sizeof(int32_t) +
          2 * (size_t)(q + 1) * sizeof(int32_t) + 2 * sizeof(uint32_t) +
-         (size_t)kFloorWG * kFloorPilots * kFloorJ * sizeof(float);
+         ((size_t)kFloorWG * kFloorPilots * kFloorJ + kFloorPilots) * sizeof(float);
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,

@@ -302,8 +302,8 @@ def test_overflow_with_sparse_active_list(first_mode):
         assert int(wsk[wsn:].count_nonzero().item()) == 0, "write past the workspace"
         out.append(cand.view(n, K)[rows.long()].cpu().numpy())
         if e16 is not None:  # workspace tail: ovf list, its count, seeds — the exact-mode path must have run
-            # (after them: the floor's two miss lists + counts, two keys, the pilots' scores f32[256·512·8])
-            floor_tail = 2 * 4 * (max_q + 1) + 8 + 4 * 256 * 512 * 8
+            # (after them: the floor's two miss lists + counts, two keys, the pilots' scores f32[1024·512·8 + 512])
+            floor_tail = 2 * 4 * (max_q + 1) + 8 + 4 * (1024 * 512 * 8 + 512)
             o = wsn - floor_tail - 4 - 4 * max_q
             assert int(wsk[o:o + 4].view(torch.int32).item()) > 0
     assert np.array_equal(out[0], out[1])

@@ -2,7 +2,7 @@
 the floor off (0) and by default (-1), interleaved, at the full query count and at one rank's share of N = 8
 (41,344 queries); reports median HIP-event times, the pilots' floor, the second pass's miss count (read from the
 workspace tail) and whether the candidates are identical.
-usage: python tools/floor_pass_ab.py [reps]"""
+usage: [AB_SIZES=n1,n2] python tools/floor_pass_ab.py [reps]"""
 import os as _os_dbg
 _os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
@@ -28,9 +28,10 @@ nd, nr = r.n_domains, r.n_ranges
 st = torch.cuda.current_stream().cuda_stream
 emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
 call("fwav_emb16_from_emb", r.emb.data_ptr(), nd, emb16.data_ptr(), st)
-TAIL = 4 * 256 * 512 * 8 + 8  # after the second miss list's count: two floor keys, the pilots' scores
+TAIL = 4 * (1024 * 512 * 8 + 512) + 8  # after the second miss list's count: two floor keys, the pilots' scores
 CONFIGS = [(0, 0.0), (-1, 0.0), (2, 1.0), (2, 3.0), (2, 10.0), (2, 20.0)]  # (mode, value): off, default, ranks
-for nq in (nr, 41344):
+SIZES = [int(x) for x in os.environ.get("AB_SIZES", f"{nr},41344").split(",")]  # query counts (first nq ranges)
+for nq in SIZES:
     active = torch.arange(nq, dtype=torch.int32, device="cuda")
     n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
     wsn = size_call("fwav_sim_topk_workspace_size", nq, nd, 64)
