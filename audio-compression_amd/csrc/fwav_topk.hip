@@ -2333,11 +2333,12 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
 #ifndef FWAV_TOPK_FLOOR
 #define FWAV_TOPK_FLOOR 1
 #endif
-// The second pass costs one round of cold table pieces (≈ 1.5 ms whatever its size: a piece's cost is the rise of its
-// limit from nothing), so the floor pays only where it saves more than that: cfg2 (330,750 queries) 18.02 → 16.82 ms,
-// but one rank's share at N = 8 (41,344) 3.46 → 4.45 ms (tools/floor_pass_ab.py, profiles/r05/floor_pass_ab.log)
+// The later passes cost a round of table pieces whatever their size (≈ 0.5–1 ms: a piece's cost is mostly the rise
+// of its limit), so the floor pays only where it saves more than that (tools/floor_pass_ab.py, pilots' 10th-smallest
+// estimate, same box): 330,750 queries 18.15 → 15.90 ms, 165,375 9.70 → 8.65, 82,688 6.14 → 5.33, but 41,344 (one
+// rank's share at N = 8) 3.40 → 3.94 (profiles/r05/floor_pass_ab.log, floor_pass_ab_mid.log)
 #ifndef FWAV_TOPK_FLOOR_MINQ
-#define FWAV_TOPK_FLOOR_MINQ 262144
+#define FWAV_TOPK_FLOOR_MINQ 65536
 #endif
 #ifndef FWAV_TOPK_FLOOR_MIND
 #define FWAV_TOPK_FLOOR_MIND 65536
@@ -2349,7 +2350,7 @@ constexpr int kFloorPilots = 512;  // pilot queries (evenly spaced over the acti
 constexpr int kFloorWG = 1024;     // k_floor_pilot workgroups, each over a 1/kFloorWG slice of the sampled domains
 constexpr int kFloorJ = 8;         // the pilot's estimate: its j-th best score over every (K/j)-th domain ≈ its K-th
 #ifndef FWAV_TOPK_FLOOR_RANK
-#define FWAV_TOPK_FLOOR_RANK 5     // the floor: the pilots' RANK-th smallest estimate (≈ their 1 % quantile)
+#define FWAV_TOPK_FLOOR_RANK 10    // the floor: the pilots' RANK-th smallest estimate (≈ their 2 % quantile)
 #endif
 // second pass: up to kFloorSplit blocks (of 256 misses) split into FWAV_TOPK_FLOOR_P2 pieces, any further ones
 // whole-table (a floor that cut more than 5 % of cfg2's queries)
