@@ -47,8 +47,9 @@
     defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || defined(FWAV_TOPK_CVACC) || defined(FWAV_TOPK_CW) || \
     defined(FWAV_TOPK_CWPE) || defined(FWAV_TOPK_DEBUG) || defined(FWAV_TOPK_DELTA) || defined(FWAV_TOPK_EXGROW) || \
     defined(FWAV_TOPK_EXTSEED) || defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_FLOOR) || \
-    defined(FWAV_TOPK_FLOOR_MIND) || defined(FWAV_TOPK_FLOOR_MINQ) || defined(FWAV_TOPK_FLOOR_P2) || \
-    defined(FWAV_TOPK_G) || defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
+    defined(FWAV_TOPK_FLOOR_MAXD) || defined(FWAV_TOPK_FLOOR_MIND) || defined(FWAV_TOPK_FLOOR_MINQ) || \
+    defined(FWAV_TOPK_FLOOR_P2) || defined(FWAV_TOPK_FLOOR_RANK) || defined(FWAV_TOPK_G) || \
+    defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
     defined(FWAV_TOPK_INTERLEAVE) || defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_MERGE_WG) || \
     defined(FWAV_TOPK_MSKIP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
     defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SETSTATS) || \
@@ -2343,6 +2344,12 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
 #ifndef FWAV_TOPK_FLOOR_MIND
 #define FWAV_TOPK_FLOOR_MIND 65536
 #endif
+// ... and tables of at most FWAV_TOPK_FLOOR_MAXD domains: the later passes' pieces grow with the table, and at cfg4's
+// 86.4 M domains the second pass took 204 ms after a 511 ms first pass (a 262,144-query search, profiles/r05/
+// kernel_stats_bench_cfg2.txt: the cfg4 affine-roofline extra of bench.py)
+#ifndef FWAV_TOPK_FLOOR_MAXD
+#define FWAV_TOPK_FLOOR_MAXD (int64_t(1) << 22)
+#endif
 #ifndef FWAV_TOPK_FLOOR_P2
 #define FWAV_TOPK_FLOOR_P2 16  // the second pass's table pieces per split block
 #endif
@@ -2668,7 +2675,8 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     // again without it (the second pass: base geometry, its blocks split in kFloorPieces table pieces).
     const int fmode = floor_mode();
     const bool use_floor = !stats_first && fmode != 0 && K <= 64 &&
-                           (fmode > 0 || (max_q >= (int64_t)FWAV_TOPK_FLOOR_MINQ && nd >= (int64_t)FWAV_TOPK_FLOOR_MIND));
+                           (fmode > 0 || (max_q >= (int64_t)FWAV_TOPK_FLOOR_MINQ && nd >= (int64_t)FWAV_TOPK_FLOOR_MIND &&
+                                          nd <= (int64_t)FWAV_TOPK_FLOOR_MAXD));
     FloorCtl fl{nullptr, nullptr, nullptr};
     if (use_floor) {
       (void)hipMemsetAsync(n_miss, 0, sizeof(int32_t), st);

@@ -50,7 +50,7 @@ int fwav_debug_topk_geometry(int wide);
 int64_t fwav_debug_topk_qb(int geo);
 /* Diagnostic override of the fp16 search's speculative floor (a first pass's band limits start at a floor guessed from
  * pilot queries; the queries it cuts are searched again without it): −1 = the default (first passes of at least
- * 65,536 queries over at least 65,536 domains), 0 = never, 1 = every first pass, at the floor `value` (a filter score;
+ * 65,536 queries over 65,536 to 4 Mi domains), 0 = never, 1 = every first pass, at the floor `value` (a filter score;
  * above a query's K-th score it sends the query to the second pass), 2 = every first pass, floor from the pilots
  * (`value` ≥ 1: the pilots' value-th smallest estimate instead of the default rank), 3 = as 1, and the second pass
  * at the same floor (every query the first pass cuts is cut again: the floor-free third pass takes them).

@@ -59,13 +59,15 @@ def main():
                              "hbm_bytes_per_launch": (2.0 * f + w) * 1024.0}
     out = {"formula": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per dispatch (gfx950 FETCH_SIZE half-count correction)",
            "config": a.config, "source": a.source, "kernels": kernels}
-    # per pattern: the kernel of the bench's own steps — the most dispatches among those that moved any bytes (the
-    # cfg4 affine-roofline search and the empty overflow relaunches also match the pattern)
+    # per pattern: the dominant kernel of the bench's own steps (the PMC passes run with --no-extras) — the one that
+    # moves the most bytes per dispatch: the search's first pass, not the floor's later passes or the overflow
+    # relaunches that also match the pattern
     for pat, key in KEYS.items():
-        cands = [(v["dispatches"], v["hbm_bytes_per_launch"]) for k, v in kernels.items()
+        cands = [(v["hbm_bytes_per_launch"], k) for k, v in kernels.items()
                  if pat in k and v["hbm_bytes_per_launch"] > 1e6]
         if cands:
-            out[key] = max(cands)[1]
+            out[key] = max(cands)[0]
+            out[key.replace("_bytes_per_launch", "_kernel")] = max(cands)[1]
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):
