@@ -547,8 +547,8 @@ constexpr int k16QB = 32 * k16Waves * k16Sets;  // queries per block (one workgr
 #endif
 // a first pass's table pieces per split block (merge: P·(C − 64) keys per query at most) ...
 constexpr int kPlanMaxPieces = FWAV_TOPK_MAXP;
-// ... and any plan's, the floor's second pass included (k_merge_pieces is instantiated for ≤ 8 and ≤ 16 pieces)
-constexpr int kMaxPieces = 16;
+// ... and any plan's, the floor's later passes included (k_merge_pieces is instantiated for ≤ 8, 16 and 32 pieces)
+constexpr int kMaxPieces = 32;
 static_assert(kPlanMaxPieces <= kMaxPieces, "first-pass plans stay within the merge's widest instantiation");
 
 // Work plan of the fp16 search.  The n_blocks query blocks are items of one launch, dispatched in order: the first
@@ -2653,7 +2653,9 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       gkeys, act, nact, rt, P, K, cand, ovf1, n_ovf1, share, emb, q_offset, sp, ties, fl)
 #define FWAV_MERGE(QB_, HL_)                                                                                    \
   do {                                                                                                          \
-    if (pl.P <= 8) FWAV_MERGE_MP(QB_, HL_, 8); else FWAV_MERGE_MP(QB_, HL_, kMaxPieces);                        \
+    if (pl.P <= 8) FWAV_MERGE_MP(QB_, HL_, 8);                                                                  \
+    else if (pl.P <= 16) FWAV_MERGE_MP(QB_, HL_, 16);                                                           \
+    else FWAV_MERGE_MP(QB_, HL_, kMaxPieces);                                                                   \
   } while (0)
         if (g == kGeoWide) {
           if (mode1 == kModeHL) FWAV_MERGE(kWideQB, true); else FWAV_MERGE(kWideQB, false);
