@@ -131,14 +131,16 @@ def product_lib() -> C.CDLL:
 
 def debug_lib() -> C.CDLL:
     """libfwav_debug.so (include/fwav_debug.h): the same entry points plus the search's test knobs; tests only.
-    FWAV_DEBUG_TOPK_FLOOR="mode[:value]" sets fwav_debug_topk_floor when it loads (same-box A/Bs of whole programs,
-    e.g. bench.py under FWAV_DEBUG_LIBRARY=1)."""
+    FWAV_DEBUG_TOPK_FLOOR="mode[:value]" / FWAV_DEBUG_TOPK_GEOMETRY=g set fwav_debug_topk_floor / _geometry when it
+    loads (same-box A/Bs of whole programs, e.g. bench.py under FWAV_DEBUG_LIBRARY=1)."""
     if "debug" not in _libs:
         _libs["debug"] = _load(DEBUG_LIB_PATH, {**SIGNATURES, **DEBUG_SIGNATURES})
         fl = os.environ.get("FWAV_DEBUG_TOPK_FLOOR")
         if fl:
             mode, _, value = fl.partition(":")
             _libs["debug"].fwav_debug_topk_floor(int(mode), float(value or 0.0))
+        if os.environ.get("FWAV_DEBUG_TOPK_GEOMETRY"):
+            _libs["debug"].fwav_debug_topk_geometry(int(os.environ["FWAV_DEBUG_TOPK_GEOMETRY"]))
     return _libs["debug"]
 
 
