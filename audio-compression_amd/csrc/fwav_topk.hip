@@ -43,10 +43,11 @@
 #if !defined(FWAV_DEBUG_API) && (defined(FWAV_TOPK_ABL) || defined(FWAV_TOPK_APPOFF) || defined(FWAV_TOPK_CAP) || \
     defined(FWAV_TOPK_CB) || defined(FWAV_TOPK_CENT) || defined(FWAV_TOPK_CENTSTATS) || \
     defined(FWAV_TOPK_CENTWIDE) || defined(FWAV_TOPK_CENT_HL) || defined(FWAV_TOPK_CENT_L2OFF) || \
-    defined(FWAV_TOPK_CENT_MINQ) || defined(FWAV_TOPK_CG) || defined(FWAV_TOPK_CHAINS) || defined(FWAV_TOPK_CPDBL) || \
-    defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || defined(FWAV_TOPK_CVACC) || defined(FWAV_TOPK_CW) || \
-    defined(FWAV_TOPK_CWPE) || defined(FWAV_TOPK_DEBUG) || defined(FWAV_TOPK_DELTA) || defined(FWAV_TOPK_EXGROW) || \
-    defined(FWAV_TOPK_EXTSEED) || defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_FLOOR) || \
+    defined(FWAV_TOPK_CENT_MINQ) || defined(FWAV_TOPK_CFPMIN) || defined(FWAV_TOPK_CG) || \
+    defined(FWAV_TOPK_CHAINS) || defined(FWAV_TOPK_CPDBL) || defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || \
+    defined(FWAV_TOPK_CVACC) || defined(FWAV_TOPK_CW) || defined(FWAV_TOPK_CWPE) || defined(FWAV_TOPK_DEBUG) || \
+    defined(FWAV_TOPK_DELTA) || defined(FWAV_TOPK_EXGROW) || defined(FWAV_TOPK_EXTSEED) || \
+    defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_FLOOR) || \
     defined(FWAV_TOPK_FLOOR_MAXD) || defined(FWAV_TOPK_FLOOR_MIND) || defined(FWAV_TOPK_FLOOR_MINQ) || \
     defined(FWAV_TOPK_FLOOR_P2) || defined(FWAV_TOPK_FLOOR_RANK) || defined(FWAV_TOPK_G) || \
     defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
@@ -2213,6 +2214,9 @@ constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2, kGeoCentWide = 3;
 // 920 ms → centroid wide 632 ms (profiles/r04/ab_centwide_cfg4_q337500.log)
 #define FWAV_TOPK_CENTWIDE 1
 #endif
+#ifndef FWAV_TOPK_CFPMIN
+#define FWAV_TOPK_CFPMIN 3  // ... and as many with the speculative floor
+#endif
 #ifndef FWAV_TOPK_CPMIN
 #define FWAV_TOPK_CPMIN 6  // centroid geometry, up to 1.5 rounds of blocks: at least this many table pieces each
 #endif
@@ -2268,7 +2272,9 @@ static void topk_device_slots(int geo, int& cus, int& per_cu) {
 // fill in beside the lone workgroups (cfg2 A/B: 24.9 → 22.6 ms; splitting more blocks costs more than it saves,
 // since every piece restarts the rising limit: 268 blocks in 2 pieces 24.2 ms, 512 in 2 25.3 ms).  Few blocks
 // (at most half the slots) are each split into up to 8 pieces so that the table passes use the idle CUs.
-static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
+static bool floor_by_default(int64_t max_q, int64_t nd);  // (defined with the floor, below)
+// floored: whether the first pass runs with the speculative floor (−1: as the launch decides, floor_by_default)
+static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P, int floored = -1) {
   if (g_plan_rt >= 0) {  // diagnostic override
     rt = g_plan_rt;
     P = g_plan_p;
@@ -2299,7 +2305,10 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P) {
       // profiles/r04/plan_sweep_cent_cfg2.log)
       rt = (int)nb;
       int64_t p = 2 * slots / nb;
-      const int64_t pmin = (geo == kGeoCent) ? FWAV_TOPK_CPMIN : 3;
+      // With the speculative floor (§3.1b of DESIGN) no piece starts cold, and fewer, longer pieces pay: cfg2 in 3 / 4 /
+      // 6 pieces 15.72 / 15.95 / 16.02 ms, 165,375 queries 8.66 / 8.89 / 8.75 (profiles/r05/plan_floor_ab*.log)
+      const bool fl = floored < 0 ? floor_by_default(max_q, nd) : floored != 0;
+      const int64_t pmin = (geo == kGeoCent) ? (fl ? FWAV_TOPK_CFPMIN : FWAV_TOPK_CPMIN) : 3;
       if (p < pmin) p = pmin;
       P = (int)(p < kPlanMaxPieces ? p : kPlanMaxPieces);
     } else {
@@ -2378,6 +2387,12 @@ constexpr uint32_t g_floor_key = 0u;
 constexpr int g_floor_rank = FWAV_TOPK_FLOOR_RANK;
 #endif
 static int floor_mode() { return FWAV_TOPK_FLOOR ? g_floor_mode : 0; }
+// the first pass of max_q queries over nd domains runs with the floor (K ≤ 64, the fp16 search)
+static bool floor_by_default(int64_t max_q, int64_t nd) {
+  const int fmode = floor_mode();
+  return fmode != 0 && (fmode > 0 || (max_q >= (int64_t)FWAV_TOPK_FLOOR_MINQ && nd >= (int64_t)FWAV_TOPK_FLOOR_MIND &&
+                                      nd <= (int64_t)FWAV_TOPK_FLOOR_MAXD));
+}
 // second-pass plan (base geometry) for a miss list of at most max_q queries: every piece streams ≥ 16 chunks
 static void floor_plan(int64_t max_q, int64_t nd, int& rt, int& P) {
   (void)max_q;
@@ -2525,10 +2540,10 @@ static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
     const size_t n2 = (size_t)make_plan(q, rt2, P2, k16QB).items() * k16QB;
     items_q = n2 > items_q ? n2 : items_q;
   }
-  for (int geo = 0; geo < 4; ++geo) {
+  for (int geo = 0; geo < 8; ++geo) {  // each geometry with and without the floor (a debug knob may switch it)
     int rt, P;
-    host_plan_for(q, nd, geo, rt, P);
-    const int qb = geometry_qb(geo);
+    host_plan_for(q, nd, geo & 3, rt, P, geo >> 2);
+    const int qb = geometry_qb(geo & 3);
     const size_t n = (size_t)make_plan(q, rt, P, qb).items() * qb;
     items_q = n > items_q ? n : items_q;
   }
@@ -2670,15 +2685,13 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
 #undef FWAV_MERGE_MP
       }
     };
-    int rt, P;
-    host_plan_for(max_q, nd, geo, rt, P);
     // Speculative floor (FloorCtl): from the exact scores of kFloorPilots evenly spaced queries against every
-    // stride-th domain (k_floor_pilot), a guess at the lowest K-th score of the search; queries it cuts are searched
-    // again without it (the second pass: base geometry, its blocks split in kFloorPieces table pieces).
+    // (K/8)-th domain (k_floor_pilot), a guess at the lowest K-th score of the search; the queries it may cut are
+    // searched again at a lower floor, and the few that one cuts without any (base geometry, table pieces).
     const int fmode = floor_mode();
-    const bool use_floor = !stats_first && fmode != 0 && K <= 64 &&
-                           (fmode > 0 || (max_q >= (int64_t)FWAV_TOPK_FLOOR_MINQ && nd >= (int64_t)FWAV_TOPK_FLOOR_MIND &&
-                                          nd <= (int64_t)FWAV_TOPK_FLOOR_MAXD));
+    const bool use_floor = !stats_first && K <= 64 && floor_by_default(max_q, nd);
+    int rt, P;
+    host_plan_for(max_q, nd, geo, rt, P, use_floor ? 1 : 0);
     FloorCtl fl{nullptr, nullptr, nullptr};
     if (use_floor) {
       (void)hipMemsetAsync(n_miss, 0, sizeof(int32_t), st);
