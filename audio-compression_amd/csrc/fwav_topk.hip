@@ -2371,11 +2371,13 @@ constexpr int kFloorJ = 8;         // the pilot's estimate: its j-th best score 
 // second pass: up to kFloorSplit blocks (of 256 misses) split into FWAV_TOPK_FLOOR_P2 pieces, any further ones
 // whole-table (a floor that cut more than 5 % of cfg2's queries)
 constexpr int kFloorSplit = 64;
-// The second pass runs at a lower floor, the pilots' smallest estimate − kFloor2Margin (below every K-th score of cfg2:
-// the smallest of all 330,750 is 1.720, the pilots' smallest estimate ≈ 1.75), so that its table pieces do not start
-// cold either; the queries that one cuts (normally none) take a floor-free third pass.  (Full score rows for them,
-// launch_topk_large, measured 3.6 ms per launch: one workgroup per row streams it several times.)
-constexpr float kFloor2Margin = 0.06f;
+// The second pass runs at a lower floor, the pilots' smallest estimate − kFloor2Margin, meant to lie below every K-th
+// score (cfg2: the smallest of all 330,750 is 1.720; the pilots' smallest estimate is 1.75–1.85 depending on which
+// queries they are — with fwav_prune's active-list order margins of 0.06 / 0.10 still cut 11 / 15 queries, and each
+// call then paid a cold third pass: tools/diag/floor_misses.py, profiles/r05/floor_misses*.log), so that its table
+// pieces do not start cold either; the queries that one cuts (normally none) take a floor-free third pass.  (Full
+// score rows for them, launch_topk_large, measured 3.6 ms per launch: one workgroup per row streams it repeatedly.)
+constexpr float kFloor2Margin = 0.15f;
 static_assert(FWAV_TOPK_FLOOR_P2 >= 1 && FWAV_TOPK_FLOOR_P2 <= kMaxPieces, "second-pass pieces outside the merge");
 #ifdef FWAV_DEBUG_API
 static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 / 3 forced value, 2 pilot at any size
