@@ -2903,8 +2903,8 @@ int fwav_debug_topk_floor(int mode, float value) {
 // times.  *items = the launch's grid.
 int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t* count, int64_t* items) {
   FWAV_CHECK_ARG(n >= 0 && count && items && wide >= 0 && wide <= 3 &&
-                     (pieces == -1 || (pieces >= 1 && pieces <= kPlanMaxPieces)), FWAV_ERR_ARG,
-                 "fwav_debug_topk_plan_cover: bad args");
+                     (pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces)), FWAV_ERR_ARG,
+                 "fwav_debug_topk_plan_cover: bad args");  // (any plan's pieces: the floor's later passes take 16)
   const int geo = wide;  // 0 base, 1 wide, 2 centroid, 3 centroid wide
   const int W = (geo == kGeoWide || geo == kGeoCentWide) ? kWideW : (geo == kGeoCent ? kCentW : k16Waves);
   const int sets = geo == kGeoCent ? kCentQS : (geo == kGeoCentWide ? kCentWideQS : k16Sets), qb = 32 * W * sets;

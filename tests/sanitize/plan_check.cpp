@@ -59,6 +59,18 @@ int main() {
         CHECK(ws >= (size_t)items * qb * 256 * 8, "workspace %zu < %lld items x %d", ws, (long long)items, qb);
         ++plans;
       }
+      // the speculative floor's later passes (base geometry, ≤ 64 blocks in P2 table pieces, the rest whole-table) on
+      // a miss list of up to all q queries: their plan covers it and their key buffers fit the same workspace
+      const int64_t pmax = ((nd + 255) / 256) / 16;
+      const int P2 = (int)(pmax < 1 ? 1 : (pmax < 16 ? pmax : 16));
+      std::vector<int32_t> count2((size_t)q, 0);
+      int64_t it2 = -1;
+      CHECK(fwav_debug_topk_plan_cover(q, 64, P2, 0, count2.data(), &it2) == FWAV_OK, "floor plan_cover");
+      int64_t bad2 = 0;
+      for (int64_t i = 0; i < q; ++i) bad2 += (count2[i] == 1 || (P2 > 1 && count2[i] == P2)) ? 0 : 1;
+      CHECK(bad2 == 0, "floor plan nd=%lld q=%lld: %lld queries covered wrongly", (long long)nd, (long long)q,
+            (long long)bad2);
+      CHECK(fwav_sim_topk_workspace_size(q, nd, 64) >= (size_t)it2 * 256 * 256 * 8, "floor plan workspace");
     }
   }
   CHECK(fwav_debug_topk_geometry(-1) == FWAV_OK, "reset");
