@@ -222,3 +222,38 @@ def test_sdot_blas_pinned(n):
                 for a, b in ((x, x), (x, y)):
                     want = a.dot(b) if n else np.float32(0)
                     assert O.sdot_blas(a, b).view(np.uint32) == np.float32(want).view(np.uint32), (n, T)
+
+
+def test_cfg2_tuple_fixture_pinned():
+    """tests/golden/cfg2_tuples_t16.npz (every cfg2 match tuple with 16 BLAS threads, make_cfg2_tuples.py) against
+    the oracle recomputed here on 256 sampled untied rows plus 8 of its numpy-ranked tie rows: same embedding table
+    (digest), same tuples bit for bit."""
+    import hashlib
+    import json
+    import os
+
+    import threadpoolctl
+
+    from fwav import synth
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "cfg2_tuples_t16.npz"))
+    par = json.loads(str(fx["params"]))
+    sig, _, _ = synth.make_config_signal("cfg2")
+    rs, step = O.geometry(par["tile"])
+    vm = O.voiced_detection(sig, 2 * rs, par["energy_thresh"])
+    ranges, _ = O.form_ranges(sig, vm, rs)
+    pool = O.domain_pool(sig, par["tile"], rs, step)
+    emb = O.embed(pool)
+    assert hashlib.sha256(emb.tobytes()).hexdigest() == str(fx["emb_sha256"])
+    rng = np.random.default_rng(11)
+    tied = fx["tie_rows"]
+    rows = np.union1d(rng.choice(np.setdiff1d(np.arange(len(ranges)), tied), 256, replace=False),
+                      rng.choice(tied, 8, replace=False))
+
+    def row_scores(q):
+        with threadpoolctl.threadpool_limits(par["blas_threads"]):
+            return O.reference_row_scores(emb, q, par["blas_threads"])
+
+    cand, _, _, _ = O.topk_rows(emb, rows, par["K"], par["blas_threads"], row_scores=row_scores)
+    got = O.affine(ranges[rows], cand, pool)
+    for nm, v in zip(("idx", "s", "o", "sym", "err"), got):
+        assert np.array_equal(np.asarray(v).view(np.uint8), fx[nm][rows].view(np.uint8)), nm
