@@ -280,6 +280,8 @@ __global__ __launch_bounds__(kDecThreads) void k_decode_sum(const double* __rest
 // certain (exact check).  Zero differences give Δ_ref = 0 exactly; sums in f32's denormal or overflow range are
 // always checked.
 __host__ __device__ inline int dec_decide(double rr, double dd, double delta, double eps, double beta) {
+  // a NaN among the values (a corrupted .fwav): the reference's Δ is NaN too, and `NaN < eps` is false — it goes on
+  if (dd != dd || rr != rr) return 0;
   if (dd == 0.0) return 0.0 < eps ? 1 : 0;
   if (dd < 1e-30 || dd > 1e36 || (rr > 0.0 && (rr < 1e-30 || rr > 1e36))) return 2;
   const double b = beta + 1e-7;
@@ -750,6 +752,71 @@ int fwav_decode(const int32_t* idx, const float* s_in, const float* o_in, const 
                 void* stream) {
   return fwav_decode_from(idx, s_in, o_in, sym, nr, rs, pool, nd, iterations, eps, s_clip, s_damping, nullptr, recon_a,
                           recon_b, deltas, state, workspace, ws_bytes, stream);
+}
+
+// The whole loop to the reference's own stop (decompress_audio, fractal.py:1378-1473) in one call: fwav_decode, and
+// wherever it stopped for the exact check, fwav_decode_exact and — when the reference goes on — fwav_decode_from the
+// checked reconstruction (kept in the workspace's tail) for the iterations left.  The only decode entry that
+// synchronises its stream (once per launch of the loop: to read the state); the caller gets the final state as
+// fwav_decode's (state[0] ∈ {0, 1}, state[1] = iterations run in total, state[2] = result buffer) and
+// deltas[0 .. state[1]) = Δ per iteration.
+size_t fwav_decode_all_workspace_size(int64_t nr, int rs, int iterations) {
+  const size_t base = (fwav_decode_workspace_size(nr, rs, iterations) + 255) & ~(size_t)255;
+  return base + (size_t)(nr > 0 ? nr : 0) * (rs > 0 ? rs : 0) * sizeof(float);
+}
+
+int fwav_decode_all(const int32_t* idx, const float* s_in, const float* o_in, const uint8_t* sym, int64_t nr, int rs,
+                    const float* pool, int64_t nd, int iterations, double eps, float s_clip, double s_damping,
+                    float* recon_a, float* recon_b, double* deltas, int* state, void* workspace, size_t ws_bytes,
+                    void* stream) {
+  FWAV_CHECK_ARG(workspace && ws_bytes >= fwav_decode_all_workspace_size(nr, rs, iterations), FWAV_ERR_WORKSPACE,
+                 "fwav_decode_all: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t base = (fwav_decode_workspace_size(nr, rs, iterations) + 255) & ~(size_t)255;
+  float* init = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + base);
+  const float* from = nullptr;
+  int done = 0;
+  int h[4] = {0, 0, 0, 0};
+  for (;;) {
+    int rc = fwav_decode_from(idx, s_in, o_in, sym, nr, rs, pool, nd, iterations - done, eps, s_clip, s_damping,
+                              from, recon_a, recon_b, deltas + (iterations > 0 ? done : 0), state, workspace, base,
+                              stream);
+    if (rc) return rc;
+    if (hipMemcpyAsync(h, state, sizeof h, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) !=
+        hipSuccess) {
+      set_error("fwav_decode_all: %s", hipGetErrorString(hipGetLastError()));
+      return FWAV_ERR_HIP;
+    }
+    const int ran = h[1];
+    float* out = h[2] == 1 ? recon_b : recon_a;
+    const float* other = h[2] == 1 ? recon_a : recon_b;
+    bool resume = false;
+    if (h[0] == 2) {
+      rc = fwav_decode_exact(other, out, nr * rs, eps, ran - 1, deltas + done, state, stream);
+      if (rc) return rc;
+      int s0 = 0;
+      if (hipMemcpyAsync(&s0, state, sizeof s0, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess) {
+        set_error("fwav_decode_all: %s", hipGetErrorString(hipGetLastError()));
+        return FWAV_ERR_HIP;
+      }
+      resume = s0 == 3 && done + ran < iterations;
+      h[0] = s0 == 3 ? 0 : 1;
+    }
+    done += ran;
+    if (!resume) {
+      // the final state as fwav_decode's: stopped (1) or every iteration run (0), total iterations, result buffer
+      const int fin[4] = {h[0] == 1 ? 1 : 0, done, h[2], h[3]};
+      (void)hipMemcpyAsync(state, fin, sizeof fin, hipMemcpyHostToDevice, st);
+      if (hipStreamSynchronize(st) != hipSuccess) {
+        set_error("fwav_decode_all: %s", hipGetErrorString(hipGetLastError()));
+        return FWAV_ERR_HIP;
+      }
+      return FWAV_OK;
+    }
+    (void)hipMemcpyAsync(init, out, (size_t)nr * rs * sizeof(float), hipMemcpyDeviceToDevice, st);
+    from = init;
+  }
 }
 
 }  // extern "C"

@@ -41,21 +41,15 @@
 // the DEBUG library only (tools/ab_build.sh adds -DFWAV_DEBUG_API): a product build that sets one stops here, so
 // libfwav.so is always the measured default.
 #if !defined(FWAV_DEBUG_API) && (defined(FWAV_TOPK_ABL) || defined(FWAV_TOPK_APPOFF) || defined(FWAV_TOPK_CAP) || \
-    defined(FWAV_TOPK_CB) || defined(FWAV_TOPK_CENT) || defined(FWAV_TOPK_CENTSTATS) || \
-    defined(FWAV_TOPK_CENTWIDE) || defined(FWAV_TOPK_CENT_HL) || defined(FWAV_TOPK_CENT_L2OFF) || \
-    defined(FWAV_TOPK_CENT_MINQ) || defined(FWAV_TOPK_CFPMIN) || defined(FWAV_TOPK_CG) || \
-    defined(FWAV_TOPK_CHAINS) || defined(FWAV_TOPK_CPDBL) || defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || \
-    defined(FWAV_TOPK_CVACC) || defined(FWAV_TOPK_CW) || defined(FWAV_TOPK_CWPE) || defined(FWAV_TOPK_DEBUG) || \
-    defined(FWAV_TOPK_DELTA) || defined(FWAV_TOPK_EXGROW) || defined(FWAV_TOPK_EXTSEED) || \
-    defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_FLOOR) || \
-    defined(FWAV_TOPK_FLOOR_MAXD) || defined(FWAV_TOPK_FLOOR_MIND) || defined(FWAV_TOPK_FLOOR_MINQ) || \
-    defined(FWAV_TOPK_FLOOR_P2) || defined(FWAV_TOPK_FLOOR_RANK) || defined(FWAV_TOPK_G) || \
-    defined(FWAV_TOPK_GROW) || defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || \
-    defined(FWAV_TOPK_INTERLEAVE) || defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_MERGE_WG) || \
-    defined(FWAV_TOPK_MSKIP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
-    defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SETSTATS) || \
-    defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || \
-    defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE))
+    defined(FWAV_TOPK_CB) || defined(FWAV_TOPK_CENT) || defined(FWAV_TOPK_CENTWIDE) || defined(FWAV_TOPK_CENT_HL) || \
+    defined(FWAV_TOPK_CENT_MINQ) || defined(FWAV_TOPK_CG) || defined(FWAV_TOPK_CHAINS) || \
+    defined(FWAV_TOPK_CPDBL) || defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || defined(FWAV_TOPK_CVACC) || \
+    defined(FWAV_TOPK_CW) || defined(FWAV_TOPK_CWPE) || defined(FWAV_TOPK_DELTA) || defined(FWAV_TOPK_EXGROW) || \
+    defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_G) || defined(FWAV_TOPK_GROW) || \
+    defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || defined(FWAV_TOPK_INTERLEAVE) || \
+    defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
+    defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || \
+    defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE))
 #error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
 #endif
 
@@ -417,23 +411,7 @@ __host__ inline int first_mode(int64_t nd) {
 #ifndef FWAV_TOPK_HLPRE
 #define FWAV_TOPK_HLPRE 0
 #endif
-#ifdef FWAV_TOPK_DEBUG
-// Debug builds only (tools/ab_build.sh … -DFWAV_TOPK_DEBUG=<query>): seeds of every query and an event trace of one.
-__device__ uint32_t g_fwav_dbg[(1 << 20) + (1 << 16)];
-__device__ uint32_t g_fwav_dbg_n;
-#define FWAV_TRACE(qid, a, b, c, d)                                                         \
-  do {                                                                                    \
-    if ((qid) == FWAV_TOPK_DEBUG) {                                                       \
-      const uint32_t i_ = atomicAdd(&g_fwav_dbg_n, 1u);                                   \
-      if (i_ < (1 << 14)) {                                                               \
-        g_fwav_dbg[(1 << 20) + 4 * i_] = (a); g_fwav_dbg[(1 << 20) + 4 * i_ + 1] = (b);    \
-        g_fwav_dbg[(1 << 20) + 4 * i_ + 2] = (c); g_fwav_dbg[(1 << 20) + 4 * i_ + 3] = (d); \
-      }                                                                                   \
-    }                                                                                     \
-  } while (0)
-#else
 #define FWAV_TRACE(qid, a, b, c, d) do { } while (0)
-#endif
 
 // Diagnostic counters (fwav_debug_sim_topk only; stays nullptr in production launches), summed over waves:
 //   [0] replayed chunks  [1] firing tiles  [2] appends  [3] streaming compactions
@@ -498,12 +476,6 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 // 17.27 ms with 4 (2: 17.33 / 17.38, 6: 17.39 / 17.44, 1: +0.5 %, 3: +2.5 %), 165,375 queries 9.77 → 9.61; adding 8:
 // cfg3 179.8 → 178.3 ms, one rank's eighth and quarter within ±0.5 %
 #define FWAV_TOPK_PRIO 12
-#endif
-#ifndef FWAV_TOPK_MSKIP
-#define FWAV_TOPK_MSKIP 1  // k_merge_pieces: the radix select starts below the key bits the union shares
-#endif
-#ifndef FWAV_TOPK_MERGE_WG
-#define FWAV_TOPK_MERGE_WG 12  // k_merge_pieces: persistent 4-wave workgroups per CU (2 / 6 / 12 / unbounded: cfg2 18.51 / 17.68 / 17.39 / 17.40 ms search)
 #endif
 #ifndef FWAV_TOPK_CSHARE
 #define FWAV_TOPK_CSHARE 1  // centroid geometry: read the pieces' shared limits every group (else at window ends)
@@ -578,7 +550,7 @@ struct TopkPlan {
 };
 // Speculative band floor of a first pass (launch_topk): *key = f2key of a filter floor f on the pass's own score scale
 // (s16 or shl; 0 = no floor).  Every query's band limit starts at f, so the pass skips the rise of its limit from the
-// seed; a query whose exact K-th score does not clear f + 2δ (δ ≥ |s16 − s32|, ≥ |shl − s32|: then every exact
+// seed; a query whose exact K-th score does not clear f + δ (δ ≥ |s16 − s32|, ≥ |shl − s32|: when it does, every exact
 // top-K member had a filter score above f, and the result is exact) is listed in miss[0 .. *n_miss) for the
 // floor-free second pass instead of being emitted.
 struct FloorCtl {
@@ -587,10 +559,13 @@ struct FloorCtl {
   int32_t* n_miss;
 };
 // Whole wave: true (and the query listed for the second pass) when the floor may have cut a member of its top K:
-// fewer than K band entries, or a K-th exact score (kth: key) not above f + 2δ.
+// fewer than K band entries, or a K-th exact score (kth: key) not above f + δ.  Every domain whose filter score
+// (s16, or shl in HL mode: within δ of s32) beats f was appended, and compactions drop only what the band rule drops;
+// a member of the exact top K scores s32 ≥ the exact K-th ≥ the band's K-th > f + δ, so its filter score beat f.
+// (Round 5 tested f + 2δ: 8,225 misses per cfg2 call instead of ≈ 2/3 of that.)
 __device__ __forceinline__ bool floor_miss(uint32_t fkey, const FloorCtl& fl, int n, int K, uint64_t kth, int32_t qid) {
   if (fkey == 0u) return false;
-  const bool miss = !(n >= K && key_score(kth) > key2f(fkey) + 2.0f * kF16Delta);
+  const bool miss = !(n >= K && key_score(kth) > key2f(fkey) + kF16Delta);
   if (miss && (threadIdx.x & 63) == 0) fl.miss[atomicAdd(fl.n_miss, 1)] = qid;
   return miss;
 }
@@ -1372,14 +1347,6 @@ __device__ __forceinline__ void static_for(F&& f) {
 // for that tile: a set is scored only where some centroid of it reaches the smallest member threshold minus the
 // centroid's slack.  Exact: a tile skipped for a set holds no domain above any member's threshold.
 constexpr int kCentBatch = FWAV_TOPK_CB;
-#ifdef FWAV_TOPK_CENTSTATS
-__device__ unsigned long long g_cent_stats[4];  // experiment builds: level-1 tiles, level-2 (tile, set) pairs
-#endif
-#ifdef FWAV_TOPK_SETSTATS
-// experiment builds: per (item, query set) the ticks of its level 2 + appends, per (item, wave) the ticks waited at
-// the group barrier and the wave's whole time (s_memrealtime, 100 MHz)
-__device__ unsigned long long g_set_ticks[1 << 16], g_wave_wait[1 << 16], g_wave_total[1 << 16];
-#endif
 template <int QS>
 __device__ __forceinline__ uint64_t cent_set_mask(int s) {
   static_assert(QS == 2 || QS == 4 || QS == 8, "centroid sets: 2, 4 or 8 query sets per wave");
@@ -1499,19 +1466,6 @@ if constexpr (FWAV_TOPK_CVACC && NT <= 32) {
       if (m & cent_set_mask<QS>(s)) pend[s] |= 1ull << i;
   }
 }
-#ifdef FWAV_TOPK_CENTSTATS
-  if ((threadIdx.x & 63) == 0) {
-    unsigned long long np = 0;
-#pragma unroll
-    for (int s = 0; s < QS; ++s) np += __popcll(pend[s]);
-    atomicAdd(&g_cent_stats[0], (unsigned long long)NT);
-    atomicAdd(&g_cent_stats[1], np);
-  }
-#endif
-#ifdef FWAV_TOPK_CENT_L2OFF
-#pragma unroll
-  for (int s = 0; s < QS; ++s) pend[s] = 0ull;
-#endif
 }
 
 template <int C, bool STATS, int MODE, int W = k16Waves, int G = kGroup, int QS = k16Sets, bool CENT = false>
@@ -1625,15 +1579,6 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
           (int64_t)((__builtin_amdgcn_readfirstlane((int)sm.qrow[(wave * QS + s) * 32]) - kSeedHalf) >> 5) << 5;
       const float seed = seed_limit<MODE>(emb16, nd, b[s], sm.qrow[(wave * QS + s) * 32 + col], wbase, K);
       if (upd[s]) thf[s] = seed;
-#ifdef FWAV_TOPK_EXTSEED
-      // experiment builds: a host-computed lower bound per active query (gstats reinterpreted as float[n_active])
-      if (upd[s] && gstats != nullptr)
-        thf[s] = fmaxf(thf[s], reinterpret_cast<const float*>(gstats)[slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb, QB)]);
-#endif
-#ifdef FWAV_TOPK_DEBUG
-      if (upd[s] && sm.qrow[(wave * QS + s) * 32 + col] < (1 << 19))
-        g_fwav_dbg[sm.qrow[(wave * QS + s) * 32 + col] + (h << 19)] = __float_as_uint(seed);
-#endif
       if (STATS && (dbg & 32768) && gstats != nullptr && h == 0 && upd[s])  // diagnostics: the seeds
         gstats[16 + slot_query(block, qslot0 + (wave * QS + s) * 32 + col, plan.nb, QB)] = __float_as_uint(seed);
     }
@@ -1705,11 +1650,6 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   if (ngroups > 0) issue_group(0);
 
   int sink = 0;     // ablation builds: keeps the MFMA / fold results of dbg 512/1024 alive
-#ifdef FWAV_TOPK_SETSTATS
-  unsigned long long wait_ticks = 0;
-  const unsigned long long t_all0 = __builtin_amdgcn_s_memrealtime();
-  unsigned long long set_ticks[QS] = {};  // per set position, ticks of level 2 + appends
-#endif
   int nfired[QS];  // wave-uniform FIFO tail: chunks recorded in sm.fired[group] so far
   ReplayCursor cur[QS];
   int qcnt[QS];    // this lane's entries in its query's two-ended buffer (h = 0: front, h = 1: back)
@@ -1732,13 +1672,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       if (STATS) stat_add(12, __builtin_amdgcn_s_memrealtime() - t_b0);
       if (FWAV_TOPK_PRIO & 4) __builtin_amdgcn_s_setprio(0);
-#ifdef FWAV_TOPK_SETSTATS
-      const unsigned long long t_w0 = __builtin_amdgcn_s_memrealtime();
-#endif
       if (!(ABL && (dbg & 16384))) __builtin_amdgcn_s_barrier();  // 16384: own DMA wait, no barrier
-#ifdef FWAV_TOPK_SETSTATS
-      wait_ticks += __builtin_amdgcn_s_memrealtime() - t_w0;
-#endif
       asm volatile("" ::: "memory");
     }
     const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1791,13 +1725,6 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       // memory round trip per batch, as the base geometry's replays) and appended.
       static_for<QS>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-#ifdef FWAV_TOPK_SETSTATS
-        const unsigned long long t_s0 = __builtin_amdgcn_s_memrealtime();
-        struct TickAdd {
-          unsigned long long t0, *dst;
-          __device__ ~TickAdd() { *dst += __builtin_amdgcn_s_memrealtime() - t0; }
-        } tick_add{t_s0, &set_ticks[s]};
-#endif
         using TMask = uint64_t;  // (32-bit masks for ≤ 32-tile groups: 17.15 vs 16.88 ms)
         TMask pm = (TMask)pend[s];
         TMask pass = 0;  // HL: tiles whose s16 passes the set's stream threshold
@@ -1905,14 +1832,6 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     }
   }
   const unsigned long long t_final = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
-#ifdef FWAV_TOPK_SETSTATS
-  if (CENT && lane == 0 && blockIdx.x * W + wave < (1 << 16) && blockIdx.x * NG + NG <= (1 << 16)) {
-#pragma unroll
-    for (int s = 0; s < QS; ++s) g_set_ticks[blockIdx.x * NG + lid[s]] += set_ticks[s];
-    g_wave_wait[blockIdx.x * W + wave] = wait_ticks;
-    g_wave_total[blockIdx.x * W + wave] = __builtin_amdgcn_s_memrealtime() - t_all0;
-  }
-#endif
   // the final pass reads the counts from LDS (same wave: program order)
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
@@ -1993,17 +1912,28 @@ __device__ __forceinline__ void merge_band(const uint64_t* __restrict__ sw, int 
     const float4 x = qp[i];
     qv[4 * i] = x.x; qv[4 * i + 1] = x.y; qv[4 * i + 2] = x.z; qv[4 * i + 3] = x.w;
   }
+  // rescore two slots at a time (8 row loads in flight per lane; all E at once held 4·E float4 rows and doubled the
+  // kernel's registers)
 #pragma unroll
-  for (int j = 0; j < E; ++j) {
-    if (v[j] != 0ull) {
-      const int32_t d = key_idx(v[j]);
-      const float4* rp = reinterpret_cast<const float4*>(emb + (int64_t)d * 16);
-      float4 row[4];
+  for (int j0 = 0; j0 < E; j0 += 2) {
+    float4 row[2][4];
+    int32_t dd[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) row[i] = rp[i];
-      const float acc = sgemv16([&](int k) { return f4c(row[k >> 2], k & 3); }, [&](int k) { return qv[k]; },
-                                sgemv_kind((uint32_t)d, sp));
-      v[j] = make_key(acc, d);
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = j0 + jj < E ? j0 + jj : E - 1;
+      dd[jj] = (j0 + jj < E && v[j] != 0ull) ? key_idx(v[j]) : 0;
+      const float4* rp = reinterpret_cast<const float4*>(emb + (int64_t)dd[jj] * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) row[jj][i] = rp[i];
+    }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = j0 + jj;
+      if (j < E && v[j] != 0ull) {
+        const float acc = sgemv16([&](int k) { return f4c(row[jj][k >> 2], k & 3); }, [&](int k) { return qv[k]; },
+                                  sgemv_kind((uint32_t)dd[jj], sp));
+        v[j] = make_key(acc, dd[jj]);
+      }
     }
   }
   wave_sort_desc<E>(v);
@@ -2032,6 +1962,13 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
                                             int64_t q_offset, const SgemvSplit& sp, int32_t* __restrict__ ties,
                                             uint32_t fkey, const FloorCtl& fl);
 
+// k_merge_pieces' union: the pieces' bands hold n = Σ counts entries (cfg2: mean 174, max 268 over 60,416 queries;
+// those above the shared limit Lk mean 163; the band kept after the select mean 78, max 113: tools/diag/
+// merge_inputs.py, profiles/r06/merge_inputs_cfg2.log).  The entries above Lk are compacted into the wave's LDS row
+// and, up to kMergeFast·64 of them, selected from registers; a wider union (long runs of near-equal scores) is
+// selected by re-reading it from L2 once per key bit instead, so the register budget — and the occupancy — no longer
+// scale with the widest plan's P·(C − 64).
+constexpr int kMergeFast = 8;
 template <int C, int QB, bool HL, int MP>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
@@ -2045,13 +1982,14 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
   if (plan.R == 0 || plan.halves) return;
   const int lane = threadIdx.x & 63;
-  __shared__ uint64_t stage[4][C];
+  __shared__ uint64_t stage[4][kMergeFast * 64];  // per wave: the union above Lk, then the band (≤ C of it)
   uint64_t* sw = stage[threadIdx.x >> 6];
-  // persistent waves (each looping over split-block queries; FWAV_TOPK_MERGE_WG workgroups per CU).  One workgroup
-  // per 4 queries measured the same (cfg2 search 17.40 vs 17.39 ms; 2 / 6 per CU: 18.51 / 17.68,
-  // profiles/r05/ab_merge_persistent.log): the merge (1.1 ms at cfg2, all 330,750 queries in 6 pieces) is bound by
-  // reading the pieces' bands, not by dispatch (profiles/r05/merge_sq_cfg2.log)
-  for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < plan.R * QB; w += (int64_t)gridDim.x * 4)
+  // one wave per split-block query.  (Persistent waves looping over the queries measured the same, cfg2 search 17.40
+  // vs 17.39 ms, profiles/r05/ab_merge_persistent.log, but the loop made the compiler hoist per-lane invariants of
+  // the body out of it: 131 VGPRs, 3 waves per SIMD.)
+  // (wave-uniform values in scalar registers: the query's row, limit and addresses load through the scalar cache)
+  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (w < plan.R * QB)
     merge_query<C, QB, HL, MP>(plan, w, lane, sw, gkeys_all, active, n_active, K, cand, ovf_list, n_ovf, share, emb,
                                q_offset, sp, ties, fkey, fl);
 }
@@ -2066,93 +2004,131 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
                                             int64_t q_offset, const SgemvSplit& sp, int32_t* __restrict__ ties,
                                             uint32_t fkey, const FloorCtl& fl) {
   constexpr int E = C / 64;
+  constexpr int kBit0 = HL ? 0 : 12;  // the select's resolution (S16 needs the K-th only at ≈ 2^-11)
   const int64_t block = plan.F + w / QB;
   const int ql = (int)(w % QB);
   const int64_t qq = slot_query(block, ql, plan.nb, QB);
   if (qq >= n_active) return;
   const int P = plan.P;
-  const uint64_t* kqs[MP];
-  int cnt[MP + 1];  // prefix of the pieces' band counts
+  // piece headers ((overflow key << 32) | count), lane p < P loading piece p's: one vector load for all of them
+  // key region of piece p: base0 + p·pstride (item_of is linear in the piece)
+  const int64_t base0 = ((int64_t)plan.item_of(block, 0) * QB + ql) * C;
+  const int64_t pstride = (plan.item_of(block, 1) - plan.item_of(block, 0)) * (int64_t)QB * C;
+  const uint64_t hdr = lane < P ? gkeys_all[base0 + (int64_t)lane * pstride + C - 1] : 0ull;
+  const uint32_t Lk = __builtin_amdgcn_readfirstlane(share[qq]);
+  const int32_t qid = __builtin_amdgcn_readfirstlane(active[qq]);
+  // prefix of the counts (wave-uniform) and the largest overflow flag
+  int pre[MP + 1];
   uint32_t seed = 0u;
-  cnt[0] = 0;
+  pre[0] = 0;
 #pragma unroll
   for (int p = 0; p < MP; ++p) {
-    const int64_t item = plan.item_of(block, p < P ? p : 0);
-    kqs[p] = gkeys_all + ((size_t)item * QB + ql) * C;
-    const uint64_t hdr = p < P ? kqs[p][C - 1] : 0ull;
-    seed = max(seed, (uint32_t)(hdr >> 32));
-    cnt[p + 1] = cnt[p] + (int)(uint32_t)hdr;
+    const uint64_t h = p < P ? (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)hdr, p) |
+                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hdr >> 32), p) << 32)
+                             : 0ull;
+    seed = max(seed, (uint32_t)(h >> 32));
+    pre[p + 1] = pre[p] + (int)(uint32_t)h;
   }
-  const int n = cnt[MP];
-  const uint32_t Lk = share[qq];
-  const int32_t qid = active[qq];
-  // Load the union (entries above the shared limit) into registers, all loads issued together, take its K-th largest
-  // key T by a greedy bitwise select and keep the band above T − margin (the pieces' own limits only know their local
-  // K-th, which for many pieces lies far below the query's)
-  constexpr int kU = (C - 64) * MP / 64;  // union entries per lane at most
-  const int nu = (n + 63) >> 6;                   // registers in use (wave-uniform)
-  uint64_t x[kU];
+  const int n = pre[MP];
+  // entry e of the union: piece p (pre[p] ≤ e < pre[p + 1]) at offset e − pre[p]; 0 past the end
+  auto entry = [&](int e) -> uint64_t {
+    int p = 0, start = 0;
 #pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    x[u] = 0ull;
-    if (u >= nu || seed != 0u) continue;
-    const int e = u * 64 + lane;
-    int p = 0;
-#pragma unroll
-    for (int pp = 1; pp < MP; ++pp) p += e >= cnt[pp] ? 1 : 0;
-    const uint64_t y = e < n ? kqs[p][e - cnt[p]] : 0ull;
-    x[u] = (uint32_t)(y >> 32) > Lk ? y : 0ull;
-  }
-  int m = 0;
-#pragma unroll
-  for (int u = 0; u < kU; ++u)
-    if (u < nu) m += __popcll(__ballot(x[u] != 0ull));
-  uint32_t L = Lk;
-  if (seed == 0u && m > K) {
-    uint32_t T = 0;
-    int top = 31;
-    if (FWAV_TOPK_MSKIP) {
-      // the bits every key of the union shares decide nothing: start the select below them (the greedy select takes
-      // each shared 1 bit and leaves each shared 0 bit, so T = the shared prefix there)
-      uint32_t a = ~0u, o = 0u;
-#pragma unroll
-      for (int u = 0; u < kU; ++u)
-        if (u < nu && x[u] != 0ull) {
-          a &= (uint32_t)(x[u] >> 32);
-          o |= (uint32_t)(x[u] >> 32);
-        }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        a &= (uint32_t)__shfl_xor((int)a, off);
-        o |= (uint32_t)__shfl_xor((int)o, off);
+    for (int pp = 1; pp < MP; ++pp)
+      if (pp < P && e >= pre[pp]) {
+        p = pp;
+        start = pre[pp];
       }
-      const uint32_t d = a ^ o;
-      top = d == 0u ? -1 : 31 - __builtin_clz(d);
-      T = (top < 0 ? a : a & ~((2u << top) - 1u)) & ~((1u << (HL ? 0 : 12)) - 1u);  // the select's resolution
-    }
-    for (int bit = top; bit >= (HL ? 0 : 12); --bit) {
-      const uint32_t Tc = T | (1u << bit);
-      int c = 0;
-#pragma unroll
-      for (int u = 0; u < kU; ++u)
-        if (u < nu) c += __popcll(__ballot((uint32_t)(x[u] >> 32) >= Tc));
-      if (c >= K) T = Tc;
-    }
-    L = max(L, f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta));
-  }
-  // the band above L, compacted into the wave's LDS row, then into v (slot j·64 + lane)
+    return e < n ? gkeys_all[base0 + (int64_t)p * pstride + (e - start)] : 0ull;
+  };
+  const int nu = (n + 63) >> 6;  // 64-entry rows of the union (wave-uniform)
+  uint32_t L = Lk;
   int mb = 0;
+  if (seed == 0u) {
+    // the union's entries above Lk, compacted into the wave's LDS row (kMergeFast rows of loads in flight: one
+    // memory round trip for a union of up to kMergeFast·64 entries), with the key bits they all share (a AND, o OR)
+    int m = 0;
+    uint32_t a = ~0u, o = 0u;
+    for (int u0 = 0; u0 < nu; u0 += kMergeFast) {
+      uint64_t y[kMergeFast];
 #pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    if (u < nu) {  // (no early break: the loop must unroll to keep x[] in registers)
-      const bool keep = x[u] != 0ull && (uint32_t)(x[u] >> 32) > L;
-      const uint64_t bm = __ballot(keep);
-      const int pos = mb + __popcll(bm & ((1ull << lane) - 1ull));
-      if (keep && pos < C) sw[pos] = x[u];
-      mb += __popcll(bm);
+      for (int i = 0; i < kMergeFast; ++i) y[i] = u0 + i < nu ? entry((u0 + i) * 64 + lane) : 0ull;
+#pragma unroll
+      for (int i = 0; i < kMergeFast; ++i) {
+        const bool in = (uint32_t)(y[i] >> 32) > Lk;
+        const uint64_t bm = __ballot(in);
+        const int pos = m + __popcll(bm & ((1ull << lane) - 1ull));
+        if (in) {
+          if (pos < kMergeFast * 64) sw[pos] = y[i];
+          a &= (uint32_t)(y[i] >> 32);
+          o |= (uint32_t)(y[i] >> 32);
+        }
+        m += __popcll(bm);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      a &= (uint32_t)__shfl_xor((int)a, off);
+      o |= (uint32_t)__shfl_xor((int)o, off);
+    }
+    const uint32_t d = a ^ o;
+    const int top = d == 0u ? -1 : 31 - __builtin_clz(d);
+    uint32_t T = (top < 0 ? a : a & ~((2u << top) - 1u)) & ~((1u << kBit0) - 1u);
+    const int mu = (m + 63) >> 6;
+    if (m <= kMergeFast * 64) {
+      // the usual case: the union above Lk in registers; its K-th key T by a greedy bitwise select that starts below
+      // the bits every entry shares, and the band above T − margin compacted back into the LDS row
+      uint64_t x[kMergeFast];
+#pragma unroll
+      for (int u = 0; u < kMergeFast; ++u) x[u] = u * 64 + lane < m ? sw[u * 64 + lane] : 0ull;
+      if (m > K) {
+        for (int bit = top; bit >= kBit0; --bit) {
+          const uint32_t Tc = T | (1u << bit);
+          int c = 0;
+#pragma unroll
+          for (int u = 0; u < kMergeFast; ++u)
+            if (u < mu) c += __popcll(__ballot((uint32_t)(x[u] >> 32) >= Tc));
+          if (c >= K) T = Tc;
+        }
+        L = max(L, f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta));
+      }
+#pragma unroll
+      for (int u = 0; u < kMergeFast; ++u) {
+        if (u < mu) {
+          const bool keep = x[u] != 0ull && (uint32_t)(x[u] >> 32) > L;
+          const uint64_t bm = __ballot(keep);
+          const int pos = mb + __popcll(bm & ((1ull << lane) - 1ull));
+          if (keep && pos < C) sw[pos] = x[u];
+          mb += __popcll(bm);
+        }
+      }
+    } else {
+      // a wide union (long runs of near-equal scores): the same select, its entries re-read from L2 for every key bit
+#pragma unroll 1
+      for (int bit = top; bit >= kBit0; --bit) {
+        const uint32_t Tc = T | (1u << bit);
+        int c = 0;
+#pragma unroll 1
+        for (int u = 0; u < nu; ++u) {
+          const uint32_t h = (uint32_t)(entry(u * 64 + lane) >> 32);
+          c += __popcll(__ballot(h > Lk && h >= Tc));
+        }
+        if (c >= K) T = Tc;
+      }
+      L = max(L, f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta));
+#pragma unroll 1
+      for (int u = 0; u < nu; ++u) {
+        const uint64_t y = entry(u * 64 + lane);
+        const bool keep = (uint32_t)(y >> 32) > L;
+        const uint64_t bm = __ballot(keep);
+        const int pos = mb + __popcll(bm & ((1ull << lane) - 1ull));
+        if (keep && pos < C) sw[pos] = y;
+        mb += __popcll(bm);
+      }
     }
   }
   if (seed != 0u || mb > C) {
+    // a piece overflowed, or the band would not fit one sort: the exact-mode relaunch, seeded with a valid limit
     if (lane == 0) {
       const int pos = atomicAdd(n_ovf, 1);
       ovf_list[pos] = qid;
@@ -2214,12 +2190,10 @@ constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2, kGeoCentWide = 3;
 // 920 ms → centroid wide 632 ms (profiles/r04/ab_centwide_cfg4_q337500.log)
 #define FWAV_TOPK_CENTWIDE 1
 #endif
-#ifndef FWAV_TOPK_CFPMIN
-#define FWAV_TOPK_CFPMIN 3  // ... and as many with the speculative floor
-#endif
 #ifndef FWAV_TOPK_CPMIN
 #define FWAV_TOPK_CPMIN 6  // centroid geometry, up to 1.5 rounds of blocks: at least this many table pieces each
 #endif
+constexpr int kCentFloorPieces = 3;  // ... and this many with the speculative floor (profiles/r05/plan_floor_ab*.log)
 #ifndef FWAV_TOPK_CENT_HL
 #define FWAV_TOPK_CENT_HL 0  // the centroid geometry for hi/lo first passes too (cfg3: 195 vs 180 ms base)
 #endif
@@ -2308,7 +2282,7 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P, i
       // With the speculative floor (§3.1b of DESIGN) no piece starts cold, and fewer, longer pieces pay: cfg2 in 3 / 4 /
       // 6 pieces 15.72 / 15.95 / 16.02 ms, 165,375 queries 8.66 / 8.89 / 8.75 (profiles/r05/plan_floor_ab*.log)
       const bool fl = floored < 0 ? floor_by_default(max_q, nd) : floored != 0;
-      const int64_t pmin = (geo == kGeoCent) ? (fl ? FWAV_TOPK_CFPMIN : FWAV_TOPK_CPMIN) : 3;
+      const int64_t pmin = (geo == kGeoCent) ? (fl ? kCentFloorPieces : FWAV_TOPK_CPMIN) : 3;
       if (p < pmin) p = pmin;
       P = (int)(p < kPlanMaxPieces ? p : kPlanMaxPieces);
     } else {
@@ -2335,40 +2309,26 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P, i
   if (P > pmax) P = (int)(pmax > 1 ? pmax : 1);
 }
 // ---------------------------------------------------------------------------------------- speculative floor
-// A first pass of at least FWAV_TOPK_FLOOR_MINQ queries over at least FWAV_TOPK_FLOOR_MIND domains starts every band
+// A first pass of at least kFloorMinQ queries over at least kFloorMinD domains starts every band
 // limit at a floor guessed from kFloorPilots pilot queries (FloorCtl); the queries it cuts are searched again.
 // Measured (tools/seed_ab.py, profiles/r05/seed_floor_cfg2.log): cfg2's search 17.01 ms unseeded, 15.27 / 14.71 /
 // 14.12 ms with one floor of 1.80 / 1.85 / 1.88 for every query (0.05 / 0.38 / 1.7 % of the queries below it, their
 // misses not counted), 12.20 ms with each query's own exact K-th score.
-#ifndef FWAV_TOPK_FLOOR
-#define FWAV_TOPK_FLOOR 1
-#endif
 // The later passes cost a round of table pieces whatever their size (≈ 0.5–1 ms: a piece's cost is mostly the rise
 // of its limit), so the floor pays only where it saves more than that (tools/floor_pass_ab.py, pilots' 10th-smallest
 // estimate, same box): 330,750 queries 18.15 → 15.90 ms, 165,375 9.70 → 8.65, 82,688 6.14 → 5.33, but 41,344 (one
 // rank's share at N = 8) 3.40 → 3.94 (profiles/r05/floor_pass_ab.log, floor_pass_ab_mid.log)
-#ifndef FWAV_TOPK_FLOOR_MINQ
-#define FWAV_TOPK_FLOOR_MINQ 65536
-#endif
-#ifndef FWAV_TOPK_FLOOR_MIND
-#define FWAV_TOPK_FLOOR_MIND 65536
-#endif
-// ... and tables of at most FWAV_TOPK_FLOOR_MAXD domains: the later passes' pieces grow with the table, and at cfg4's
+constexpr int64_t kFloorMinQ = 65536, kFloorMinD = 65536;
+// ... and tables of at most kFloorMaxD domains: the later passes' pieces grow with the table, and at cfg4's
 // 86.4 M domains the second pass took 204 ms after a 511 ms first pass (a 262,144-query search, profiles/r05/
 // kernel_stats_bench_cfg2.txt: the cfg4 affine-roofline extra of bench.py)
-#ifndef FWAV_TOPK_FLOOR_MAXD
-#define FWAV_TOPK_FLOOR_MAXD (int64_t(1) << 22)
-#endif
-#ifndef FWAV_TOPK_FLOOR_P2
-#define FWAV_TOPK_FLOOR_P2 16  // the second pass's table pieces per split block
-#endif
+constexpr int64_t kFloorMaxD = int64_t(1) << 22;
+constexpr int kFloorP2 = 16;  // the second pass's table pieces per split block
 constexpr int kFloorPilots = 512;  // pilot queries (evenly spaced over the active list)
 constexpr int kFloorWG = 1024;     // k_floor_pilot workgroups, each over a 1/kFloorWG slice of the sampled domains
 constexpr int kFloorJ = 8;         // the pilot's estimate: its j-th best score over every (K/j)-th domain ≈ its K-th
-#ifndef FWAV_TOPK_FLOOR_RANK
-#define FWAV_TOPK_FLOOR_RANK 10    // the floor: the pilots' RANK-th smallest estimate (≈ their 2 % quantile)
-#endif
-// second pass: up to kFloorSplit blocks (of 256 misses) split into FWAV_TOPK_FLOOR_P2 pieces, any further ones
+constexpr int kFloorRank = 10;    // the floor: the pilots' kFloorRank-th smallest estimate (≈ their 2 % quantile)
+// second pass: up to kFloorSplit blocks (of 256 misses) split into kFloorP2 pieces, any further ones
 // whole-table (a floor that cut more than 5 % of cfg2's queries)
 constexpr int kFloorSplit = 64;
 // The second pass runs at a lower floor, the pilots' smallest estimate − kFloor2Margin, meant to lie below every K-th
@@ -2378,29 +2338,28 @@ constexpr int kFloorSplit = 64;
 // pieces do not start cold either; the queries that one cuts (normally none) take a floor-free third pass.  (Full
 // score rows for them, launch_topk_large, measured 3.6 ms per launch: one workgroup per row streams it repeatedly.)
 constexpr float kFloor2Margin = 0.15f;
-static_assert(FWAV_TOPK_FLOOR_P2 >= 1 && FWAV_TOPK_FLOOR_P2 <= kMaxPieces, "second-pass pieces outside the merge");
+static_assert(kFloorP2 >= 1 && kFloorP2 <= kMaxPieces, "second-pass pieces outside the merge");
 #ifdef FWAV_DEBUG_API
 static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 / 3 forced value, 2 pilot at any size
 static uint32_t g_floor_key = 0u;
-static int g_floor_rank = FWAV_TOPK_FLOOR_RANK;
+static int g_floor_rank = kFloorRank;
 #else
 constexpr int g_floor_mode = -1;
 constexpr uint32_t g_floor_key = 0u;
-constexpr int g_floor_rank = FWAV_TOPK_FLOOR_RANK;
+constexpr int g_floor_rank = kFloorRank;
 #endif
-static int floor_mode() { return FWAV_TOPK_FLOOR ? g_floor_mode : 0; }
+static int floor_mode() { return g_floor_mode; }
 // the first pass of max_q queries over nd domains runs with the floor (K ≤ 64, the fp16 search)
 static bool floor_by_default(int64_t max_q, int64_t nd) {
   const int fmode = floor_mode();
-  return fmode != 0 && (fmode > 0 || (max_q >= (int64_t)FWAV_TOPK_FLOOR_MINQ && nd >= (int64_t)FWAV_TOPK_FLOOR_MIND &&
-                                      nd <= (int64_t)FWAV_TOPK_FLOOR_MAXD));
+  return fmode != 0 && (fmode > 0 || (max_q >= kFloorMinQ && nd >= kFloorMinD && nd <= kFloorMaxD));
 }
 // second-pass plan (base geometry) for a miss list of at most max_q queries: every piece streams ≥ 16 chunks
 static void floor_plan(int64_t max_q, int64_t nd, int& rt, int& P) {
   (void)max_q;
   rt = kFloorSplit;
   const int64_t pmax = cdiv(nd, kChunk) / 16;
-  P = (int)std::max<int64_t>(1, std::min<int64_t>(FWAV_TOPK_FLOOR_P2, pmax));
+  P = (int)std::max<int64_t>(1, std::min<int64_t>(kFloorP2, pmax));
 }
 
 // Each pilot p (of kFloorPilots, 2 per thread) at active position p·n/kFloorPilots: its kFloorJ best f32 scores over
@@ -2515,7 +2474,10 @@ __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __re
                                                                uint32_t* __restrict__ floor_key) {
   __shared__ float est[kFloorPilots];
   const int p = threadIdx.x;
-  const float e = est_g[p];
+  // a NaN estimate ranks as +inf (after every number), so each place 0 … kFloorPilots − 1 has exactly one owner and
+  // both keys are always written (a non-finite one as 0: no floor)
+  const float e0 = est_g[p];
+  const float e = e0 == e0 ? e0 : INFINITY;
   est[p] = e;
   __syncthreads();
   // every pilot's place in (estimate, pilot) order: the one at place rank − 1 is the floor, the one at place 0 the
@@ -2552,6 +2514,46 @@ static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
   return items_q * k16Cap * sizeof(uint64_t);
 }
 
+// The fp16 search's workspace (K ≤ 64), in byte offsets from its start; one definition for the launch, the size query
+// and fwav_debug_sim_topk_layout (tests read the tail through it, never by arithmetic of their own).
+//   keys      u64 key buffers (f16_keys_bytes)        share   u32[q] shared band limits of split blocks
+//   ovf2      i32[q] overflow list of the HL relaunch  n_ovf2  i32 count, then seeds2 u32[q]
+//   ovf1      i32[q] overflow list of the first pass   n_ovf1  i32 count, then seeds1 u32[q]
+//   miss      i32[q] floor misses of the first pass    n_miss  i32
+//   miss2     i32[q] floor misses of the second pass   n_miss2 i32
+//   floor_key u32[2]                                    pilot   f32 pilot scores + estimates (only when the floor
+//                                                       can run: floor_by_default, or any size in the debug library)
+struct TopkLayout {
+  size_t keys, share, ovf2, n_ovf2, seeds2, ovf1, n_ovf1, seeds1, miss, n_miss, miss2, n_miss2, floor_key, pilot,
+      total;
+};
+constexpr size_t kPilotBytes = ((size_t)kFloorWG * kFloorPilots * kFloorJ + kFloorPilots) * sizeof(float);
+static TopkLayout topk_layout(int64_t max_q, int64_t nd) {
+  const size_t q = (size_t)(max_q > 0 ? max_q : 1);
+  TopkLayout L;
+  L.keys = 0;
+  L.share = f16_keys_bytes(max_q, nd);
+  L.ovf2 = L.share + 4 * q;
+  L.n_ovf2 = L.ovf2 + 4 * q;
+  L.seeds2 = L.n_ovf2 + 4;
+  L.ovf1 = L.seeds2 + 4 * q;
+  L.n_ovf1 = L.ovf1 + 4 * q;
+  L.seeds1 = L.n_ovf1 + 4;
+  L.miss = L.seeds1 + 4 * q;
+  L.n_miss = L.miss + 4 * q;
+  L.miss2 = L.n_miss + 4;
+  L.n_miss2 = L.miss2 + 4 * q;
+  L.floor_key = L.n_miss2 + 4;
+  L.pilot = L.floor_key + 8;
+#ifdef FWAV_DEBUG_API
+  const bool pilots = true;  // a debug knob may force the floor after the size query
+#else
+  const bool pilots = floor_by_default(max_q, nd);
+#endif
+  L.total = L.pilot + (pilots ? kPilotBytes : 0);
+  return L;
+}
+
 template <int C>
 static size_t topk_lds_bytes() {
   return (size_t)kTopkQ * C * sizeof(uint64_t) + 16 * kChunk * sizeof(float) + 3 * kTopkQ * sizeof(int);
@@ -2570,17 +2572,18 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       set_error("fwav_sim_topk: fp16 search needs its key workspace (fwav_sim_topk_workspace_size)");
       return FWAV_ERR_WORKSPACE;
     }
-    const size_t keys_bytes = f16_keys_bytes(max_q, nd);
     const int64_t q1 = max_q > 0 ? max_q : 1;
-    // workspace tail: two overflow lists, each list[q], count, seeds u32[q] (seeds[i] = f2key of the band limit of
-    // list[i]); the first pass's list is the last block of the workspace
-    uint32_t* share = (uint32_t*)((char*)gkeys + keys_bytes);  // u32[q]: shared band limits of split blocks
-    int32_t* ovf2 = (int32_t*)(share + q1);
-    int32_t* n_ovf2 = ovf2 + q1;
-    int32_t* ovf1 = n_ovf2 + 1 + q1;
-    int32_t* n_ovf1 = ovf1 + q1;
-    const uint32_t* seeds1 = reinterpret_cast<const uint32_t*>(n_ovf1 + 1);
-    const uint32_t* seeds2 = reinterpret_cast<const uint32_t*>(n_ovf2 + 1);
+    // workspace tail (TopkLayout): two overflow lists, each list[q], count, seeds u32[q] (seeds[i] = f2key of the
+    // band limit of list[i]), the floor's miss lists, its keys and the pilots' scores
+    const TopkLayout lay = topk_layout(max_q, nd);
+    char* const wb = reinterpret_cast<char*>(gkeys);
+    uint32_t* share = reinterpret_cast<uint32_t*>(wb + lay.share);  // u32[q]: shared band limits of split blocks
+    int32_t* ovf2 = reinterpret_cast<int32_t*>(wb + lay.ovf2);
+    int32_t* n_ovf2 = reinterpret_cast<int32_t*>(wb + lay.n_ovf2);
+    int32_t* ovf1 = reinterpret_cast<int32_t*>(wb + lay.ovf1);
+    int32_t* n_ovf1 = reinterpret_cast<int32_t*>(wb + lay.n_ovf1);
+    const uint32_t* seeds1 = reinterpret_cast<const uint32_t*>(wb + lay.seeds1);
+    const uint32_t* seeds2 = reinterpret_cast<const uint32_t*>(wb + lay.seeds2);
     (void)hipMemsetAsync(n_ovf1, 0, sizeof(int32_t), st);
     (void)hipMemsetAsync(n_ovf2, 0, sizeof(int32_t), st);
     // Geometry: k16Waves waves × k16Sets query sets of 32 per workgroup.  Measured at cfg2 (W, QS=1): W = 8
@@ -2594,14 +2597,13 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     // counter builds run the base geometry, or with dbg bit 18 the product's own (centroid) geometry
     const int geo = stats_first && !(dbg & (1 << 18)) ? kGeoBase : first_geometry(nd, max_q);
     const int mode1 = first_mode(nd);
-    // workspace after the two overflow lists: the floor's miss list (list[q], count), the floor key, the pilot scores
-    // (miss list + count of the first and of the second pass, two floor keys, the score-row / last-pass counts)
-    int32_t* miss = const_cast<int32_t*>(reinterpret_cast<const int32_t*>(seeds1 + q1));
-    int32_t* n_miss = miss + q1;
-    int32_t* miss2 = n_miss + 1;
-    int32_t* n_miss2 = miss2 + q1;
-    uint32_t* floor_key = reinterpret_cast<uint32_t*>(n_miss2 + 1);
-    float* pilot = reinterpret_cast<float*>(floor_key + 2);
+    // the floor's miss lists (first and second pass), its two keys, the pilots' scores
+    int32_t* miss = reinterpret_cast<int32_t*>(wb + lay.miss);
+    int32_t* n_miss = reinterpret_cast<int32_t*>(wb + lay.n_miss);
+    int32_t* miss2 = reinterpret_cast<int32_t*>(wb + lay.miss2);
+    int32_t* n_miss2 = reinterpret_cast<int32_t*>(wb + lay.n_miss2);
+    uint32_t* floor_key = reinterpret_cast<uint32_t*>(wb + lay.floor_key);
+    float* pilot = reinterpret_cast<float*>(wb + lay.pilot);
     // One first pass (search + merge of split blocks) over act[0 .. *nact) in geometry g with plan (rt, P) and floor
     // fl; `diag`: the debug library's counter / ablation launches may replace the search
     auto first_pass = [&](const int32_t* act, const int32_t* nact, int g, int rt, int P, FloorCtl fl, bool diag) {
@@ -2617,16 +2619,6 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       sp, ties, fl)
       bool done = false;
       (void)diag;
-#ifdef FWAV_TOPK_EXTSEED
-      if (diag && stats != nullptr && (dbg & ~(1 << 18)) == 0) {  // dbg bit 18: the product geometry
-        if (g == kGeoCent && mode1 == kModeS16)
-          k_sim_topk_f16<k16Cap, false, kModeS16, kCentW, kCentG, kCentQS, true><<<pl.items(), 64 * kCentW, 0, st>>>(
-              emb16, emb, nd, act, nact, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, 0,
-              stats, sp, ties, fl);
-        else if (mode1 == kModeHL) FWAV_FIRST(kModeHL, false, 0, stats); else FWAV_FIRST(kModeS16, false, 0, stats);
-        done = true;
-      }
-#endif
 #ifdef FWAV_DEBUG_API
       if (!done && diag && stats_first && g == kGeoCent) {
         if (mode1 == kModeHL)
@@ -2661,12 +2653,9 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
 #undef FWAV_FIRST
 #undef FWAV_FIRST_GEO
       if (pl.R > 0) {
-        // persistent merge waves: ≈ 6 per SIMD (its occupancy), each looping over split-block queries
-        int cus, per_cu;
-        topk_device_slots(g, cus, per_cu);
-        const int64_t mgrid_cap = (int64_t)cus * FWAV_TOPK_MERGE_WG;
+        // one merge wave per split-block query
 #define FWAV_MERGE_MP(QB_, HL_, MP_)                                                                            \
-  k_merge_pieces<k16Cap, QB_, HL_, MP_><<<std::min<int64_t>(cdiv(pl.R * QB_, 4), mgrid_cap), 256, 0, st>>>(     \
+  k_merge_pieces<k16Cap, QB_, HL_, MP_><<<cdiv(pl.R * QB_, 4), 256, 0, st>>>(                                 \
       gkeys, act, nact, rt, P, K, cand, ovf1, n_ovf1, share, emb, q_offset, sp, ties, fl)
 #define FWAV_MERGE(QB_, HL_)                                                                                    \
   do {                                                                                                          \
@@ -2706,7 +2695,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
         float* est = pilot + (size_t)kFloorWG * kFloorPilots * kFloorJ;
         k_floor_pilot<<<kFloorWG, 256, 0, st>>>(emb, nd, active, n_active, q_offset, stride, pilot);
         k_floor_est<<<kFloorPilots, 64, 0, st>>>(pilot, kFloorWG, j, est);
-        k_floor_reduce<<<1, kFloorPilots, 0, st>>>(est, g_floor_rank, n_active, fmode == 2 ? 0 : FWAV_TOPK_FLOOR_MINQ,
+        k_floor_reduce<<<1, kFloorPilots, 0, st>>>(est, g_floor_rank, n_active, fmode == 2 ? 0 : (int)kFloorMinQ,
                                                    floor_key);
       }
       fl = FloorCtl{floor_key, miss, n_miss};
@@ -2782,10 +2771,8 @@ size_t fwav_sim_topk_workspace_size(int64_t max_q, int64_t n_domains, int k) {
   const int64_t q = max_q > 0 ? max_q : 1;
   if (k > 64) return large_workspace_bytes(n_domains, q);
   // key buffers, shared limits u32[q], two overflow lists (list, count, seeds), the floor's two miss lists (list,
-  // count), its two keys, the pilots' scores
-  return f16_keys_bytes(q, n_domains) + (size_t)q * sizeof(uint32_t) + 2 * (size_t)(2 * q + 1) * sizeof(int32_t) +
-         2 * (size_t)(q + 1) * sizeof(int32_t) + 2 * sizeof(uint32_t) +
-         ((size_t)kFloorWG * kFloorPilots * kFloorJ + kFloorPilots) * sizeof(float);
+  // count), its two keys, the pilots' scores when the floor can run (TopkLayout)
+  return topk_layout(q, n_domains).total;
 }
 
 // Exact top-K over all nd domains for the local queries listed in active[0 .. *n_active) (device count,
@@ -2841,33 +2828,6 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t nd, const i
                           (hipStream_t)stream, (uint64_t*)workspace, make_sgemv_split(nd, 1), nullptr, dbg, stats);
 }
 
-#ifdef FWAV_TOPK_CENTSTATS
-// experiment builds: read and clear the centroid pre-filter's counters
-int fwav_debug_cent_stats(unsigned long long* host) {
-  (void)hipDeviceSynchronize();
-  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cent_stats), 4 * sizeof(unsigned long long));
-  const unsigned long long z[4] = {0, 0, 0, 0};
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_cent_stats), z, sizeof(z));
-  return FWAV_OK;
-}
-#endif
-#ifdef FWAV_TOPK_SETSTATS
-int fwav_debug_set_stats(unsigned long long* sets, unsigned long long* waits, unsigned long long* totals) {
-  (void)hipDeviceSynchronize();
-  (void)hipMemcpyFromSymbol(sets, HIP_SYMBOL(g_set_ticks), sizeof(unsigned long long) << 16);
-  (void)hipMemcpyFromSymbol(waits, HIP_SYMBOL(g_wave_wait), sizeof(unsigned long long) << 16);
-  (void)hipMemcpyFromSymbol(totals, HIP_SYMBOL(g_wave_total), sizeof(unsigned long long) << 16);
-  return FWAV_OK;
-}
-#endif
-#ifdef FWAV_TOPK_DEBUG
-int fwav_debug_dump(void* host, size_t bytes, unsigned* n_events) {
-  (void)hipDeviceSynchronize();
-  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwav_dbg), bytes);
-  (void)hipMemcpyFromSymbol(n_events, HIP_SYMBOL(g_fwav_dbg_n), sizeof(unsigned));
-  return FWAV_OK;
-}
-#endif
 // Diagnostic override of the first pass's mode: 0 = S16 (→ HL → exact relaunches), 1 = HL (→ exact), −1 = by table
 // size (default).  Every mode returns the same candidates.
 int fwav_debug_topk_mode(int mode) {
@@ -2890,7 +2850,7 @@ int fwav_debug_topk_floor(int mode, float value) {
   FWAV_CHECK_ARG((mode != 1 && mode != 3) || (value == value && value > -INFINITY && value < INFINITY), FWAV_ERR_ARG,
                  "fwav_debug_topk_floor: the forced floor must be finite");
   g_floor_mode = mode;
-  g_floor_rank = mode == 2 && value >= 1.0f && value <= (float)kFloorPilots ? (int)value : FWAV_TOPK_FLOOR_RANK;
+  g_floor_rank = mode == 2 && value >= 1.0f && value <= (float)kFloorPilots ? (int)value : kFloorRank;
   uint32_t u;
   std::memcpy(&u, &value, sizeof u);
   g_floor_key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // f2key
@@ -2945,6 +2905,18 @@ int fwav_debug_topk_plan_info(int64_t max_q, int64_t nd, int32_t* info, int64_t*
 
 // Queries per block (one workgroup's query slots) of first-pass geometry geo (0 base, 1 wide, 2 centroid).
 int64_t fwav_debug_topk_qb(int geo) { return geo >= 0 && geo <= 3 ? geometry_qb(geo) : -1; }
+
+// Byte offsets of the fp16 search's workspace regions for max_q queries over nd domains (K ≤ 64), in the order of
+// TopkLayout: keys, share, ovf2, n_ovf2, seeds2, ovf1, n_ovf1, seeds1, miss, n_miss, miss2, n_miss2, floor_key,
+// pilot, total (15 values; total = fwav_sim_topk_workspace_size of this library).
+int fwav_debug_sim_topk_layout(int64_t max_q, int64_t nd, int64_t* offsets) {
+  FWAV_CHECK_ARG(max_q >= 0 && nd > 0 && offsets, FWAV_ERR_ARG, "fwav_debug_sim_topk_layout: bad args");
+  const TopkLayout L = topk_layout(max_q > 0 ? max_q : 1, nd);
+  const size_t v[15] = {L.keys, L.share, L.ovf2, L.n_ovf2, L.seeds2, L.ovf1, L.n_ovf1, L.seeds1,
+                        L.miss, L.n_miss, L.miss2, L.n_miss2, L.floor_key, L.pilot, L.total};
+  for (int i = 0; i < 15; ++i) offsets[i] = (int64_t)v[i];
+  return FWAV_OK;
+}
 
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.

@@ -59,6 +59,8 @@ SIGNATURES = {
     "fwav_decode_partials_count": (SZ, [I64]),
     "fwav_decode_from": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, P, SZ, P]),
     "fwav_decode_exact": (I32, [P, P, I64, F64, I32, P, P, P]),
+    "fwav_decode_all_workspace_size": (SZ, [I64, I32, I32]),
+    "fwav_decode_all": (I32, [P, P, P, P, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P, SZ, P]),
     "fwav_decode_run": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, I32, F64, F32, F64, P, P, P, P, P, P]),
     "fwav_decode_reduce": (I32, [P, I64, I32, I32, I32, F64, P, P, P]),
     "fwav_decode_finish": (I32, [P, P, P, P, I64, I64, I64, I32, P, I64, I32, F64, F32, F64, P, P, P, P, P]),
@@ -75,6 +77,7 @@ DEBUG_SIGNATURES = {
     "fwav_debug_topk_plan_info": (I32, [I64, I64, P, P]),
     "fwav_debug_topk_qb": (I64, [I32]),
     "fwav_debug_topk_floor": (I32, [I32, F32]),
+    "fwav_debug_sim_topk_layout": (I32, [I64, I64, P]),
 }
 
 
@@ -185,3 +188,19 @@ def call(name: str, *args) -> int:
 
 def size_call(name: str, *args) -> int:
     return int(getattr(lib(), name)(*args))
+
+
+#: fwav_debug_sim_topk_layout's regions, in its order
+SIM_TOPK_LAYOUT = ("keys", "share", "ovf2", "n_ovf2", "seeds2", "ovf1", "n_ovf1", "seeds1", "miss", "n_miss", "miss2",
+                   "n_miss2", "floor_key", "pilot", "total")
+
+
+def sim_topk_layout(max_q: int, n_domains: int) -> dict:
+    """Byte offsets of the fp16 search's workspace regions (the debug library's fwav_debug_sim_topk_layout; every
+    region before ``pilot`` sits at the same offset in libfwav.so).  Tests and diagnostics read the tail through this,
+    never by arithmetic of their own."""
+    out = (C.c_int64 * len(SIM_TOPK_LAYOUT))()
+    rc = debug_lib().fwav_debug_sim_topk_layout(int(max_q), int(n_domains), out)
+    if rc != 0:
+        raise FwavError(f"fwav_debug_sim_topk_layout: {rc}")
+    return dict(zip(SIM_TOPK_LAYOUT, (int(v) for v in out)))

@@ -101,6 +101,7 @@ class DeviceCompressed:
     energy_partial: Optional[torch.Tensor] = None
     ties: Optional[torch.Tensor] = None  # fwav_sim_topk's tie list (keep_intermediates)
     resolved: Optional[torch.Tensor] = None  # local rows re-ranked with numpy's order (keep_intermediates)
+    search_ws: Optional[torch.Tensor] = None  # fwav_sim_topk's workspace after the call (keep_intermediates, one launch)
     n_ties: int = 0          # queries whose top K + 1 scores hold exact ties
     n_resolved: int = 0      # of those, rows re-ranked with numpy's own tie order (fwav.ties)
     empty: bool = False
@@ -358,6 +359,8 @@ def _compress_device(sig: torch.Tensor, tile_size: int, top_k: int, energy_thres
         res.ranges, res.emb, res.cand, res.active = ranges, emb, cand, active
         if m > 0 and ties is not None:
             res.ties = ties
+        if m > 0 and not sliced:
+            res.search_ws = wsk
     return res
 
 

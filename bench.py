@@ -52,9 +52,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the timed steps (profiling passes)")
     ap.add_argument("--cpu-workers", default=None, help="CPU baseline search processes (default: sweep)")
-    ap.add_argument("--streams", type=int, default=None,
+    ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams that consecutive timed calls alternate over (a call's kernels stay on one); "
-                         "default 1 at N = 1, 2 at N > 1")
+                         "the same default at every N, so that the driver's 1 -> N curve compares like with like")
     return ap.parse_args()
 
 
@@ -230,11 +230,12 @@ def main():
 
     phase = {}
     # --streams S > 1: consecutive calls alternate over S HIP streams, so that one call's search can start on the CUs
-    # the previous call's last workgroups leave idle (each call's kernels stay in order on its own stream)
-    # The N = 1 line keeps one stream so that the search's HIP-event launch time (the roofline) and rocprofv3's
-    # kernel durations measure one launch alone; two streams there measure 17.2 vs 17.8 ms per step
-    # (profiles/r05/bench_streams1.log, bench_streams2.log), with each launch's own duration then stretched by the overlap.
-    n_streams = args.streams if args.streams is not None else (1 if world == 1 else 2)
+    # the previous call's last workgroups leave idle (each call's kernels stay in order on its own stream).  Every N
+    # runs the same count (the driver's 1 -> 8 curve must compare like with like; N = 1 measured 17.2
+    # vs 17.8 ms per step with two streams vs one, profiles/r05/bench_streams{1,2}.log).  With overlapping launches
+    # a launch's own HIP-event duration is stretched by the other stream's, so the roofline is timed on extra
+    # single-stream steps after the timed region (solo_search_ms).
+    n_streams = args.streams
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(max(1, n_streams) - 1)]
     nstep = [0]
 
@@ -257,6 +258,7 @@ def main():
             def compute(s, t, k, thr, shard):
                 r = engine.compress_device(s, t, k, energy_thresh=thr, shard=shard, events=ev, defer_ties=not phases)
                 step.last = r
+                step.sig_local = s
                 return None if r.empty else dict(idx=r.idx, s=r.s, o=r.o, sym=r.sym, err=r.err, pool=r.pool,
                                                  silent=r.is_silent, wait=r.wait)
             # every rank knows the configuration's signal length; per-phase host timings (which synchronise the
@@ -341,7 +343,24 @@ def main():
     ms = dt / args.steps * 1e3
     value = nr / (dt / args.steps)
 
-    t_topk = stage_ms["sim_topk"] * 1e-3
+    # the roofline's launch time: with several streams the timed launches overlap (each one's HIP-event span includes
+    # the other stream's work), so the search is re-timed alone, on one stream, over untimed extra calls of the same
+    # shard (its kernels and outputs are those of the timed calls)
+    solo_ms = None
+    if len(streams) > 1:
+        s_loc = sig if not sharded else getattr(step, "sig_local", None)
+        if s_loc is not None:
+            solo = []
+            for i in range(6):
+                ev = {}
+                r_ = engine.compress_device(s_loc, tile, K, energy_thresh=1e-4, shard=res.shard if sharded else None,
+                                            events=ev, defer_ties=True)
+                r_.wait()
+                torch.cuda.synchronize()
+                if i:
+                    solo.append(ev["sim_topk"][0].elapsed_time(ev["sim_topk"][1]))
+            solo_ms = float(sorted(solo)[len(solo) // 2])
+    t_topk = (solo_ms if solo_ms is not None else stage_ms["sim_topk"]) * 1e-3
     flops = 2.0 * n_active * nd * 16
     achieved_tf = flops / t_topk / 1e12
     traffic, traffic_src = pmc_traffic(args.config) if not sharded else (None, None)
@@ -366,9 +385,10 @@ def main():
                                         f"that cannot reach a member's band, so `frac` is an effective rate; the "
                                         f"MFMA work actually executed is `mfma_executed`",
                      "launch_ms": t_topk * 1e3, "rank": rank,
-                     **({"note": f"{len(streams)} streams: consecutive launches overlap, so each launch's own duration "
-                                 "(launch_ms) over-states the kernel's time and `frac` under-states it; "
-                                 "roofline_rank_share times the same shard's launch alone"} if len(streams) > 1 else {})},
+                     **({"launch_ms_overlapped": stage_ms["sim_topk"],
+                         "note": f"{len(streams)} streams in the timed steps: their launches overlap, so launch_ms is "
+                                 "the same search timed alone on one stream (median of 5 extra calls); "
+                                 "launch_ms_overlapped is the timed launches' own span"} if solo_ms is not None else {})},
         "stage_ms": stage_ms,
     }
     sq = sq_summary(args.config) if not sharded else None

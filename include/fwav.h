@@ -174,7 +174,8 @@ int fwav_debug_gather_rows(const float* table, int64_t n_rows, int rs, int64_t n
  * fwav_decode_exact(prev = other buffer, next = result buffer, n_ranges·range_size, eps, t − 1, deltas, state)
  * computes the reference's Δ in its own sdot order, stores it in deltas[t − 1] and sets state[0] = 1 (the reference
  * stops) or 3 (it goes on: continue with fwav_decode_from, recon_init = a copy of the result buffer, the remaining
- * iterations).  state: int[4]; deltas: f64[iterations]. */
+ * iterations).  state: int[4]; deltas: f64[iterations].  So with state[0] = 2 fwav_decode ALONE has run fewer
+ * iterations than the reference: a caller that does not run that check loop uses fwav_decode_all (below). */
 size_t fwav_decode_workspace_size(int64_t n_ranges, int range_size, int iterations);
 int fwav_decode(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t n_ranges,
                 int range_size, const float* pool, int64_t n_domains, int iterations, double eps, float s_clip,
@@ -183,6 +184,17 @@ int fwav_decode(const int32_t* idx, const float* s, const float* o, const uint8_
 /* fwav_decode starting from the reconstruction recon_init (device f32[n_ranges·range_size], not recon_a/recon_b;
  * NULL = zeros, the reference's start) instead of zeros: the loop resumed after an exact check (iterations = the
  * iterations left). */
+/* fwav_decode run to the reference's own stop in ONE call, for callers that do not run the exact-check loop above
+ * themselves: wherever fwav_decode stops for the check it runs fwav_decode_exact and, when the reference goes on,
+ * fwav_decode_from the checked reconstruction (kept in the workspace's tail) for the iterations left.  Synchronises
+ * `stream` (to read the state after each launch of the loop) — the only decode entry point that does.  On return
+ * state[0] = 1 (stopped) or 0 (every iteration ran), state[1] = iterations run, state[2] = result buffer (0 → recon_a,
+ * 1 → recon_b), deltas[0 .. state[1]) = Δ per iteration (the reference's own Δ at a checked iteration). */
+size_t fwav_decode_all_workspace_size(int64_t n_ranges, int range_size, int iterations);
+int fwav_decode_all(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t n_ranges,
+                    int range_size, const float* pool, int64_t n_domains, int iterations, double eps, float s_clip,
+                    double s_damping, float* recon_a, float* recon_b, double* deltas, int* state, void* workspace,
+                    size_t ws_bytes, void* stream);
 int fwav_decode_from(const int32_t* idx, const float* s, const float* o, const uint8_t* sym, int64_t n_ranges,
                      int range_size, const float* pool, int64_t n_domains, int iterations, double eps, float s_clip,
                      double s_damping, const float* recon_init, float* recon_a, float* recon_b, double* deltas,

@@ -56,6 +56,11 @@ int64_t fwav_debug_topk_qb(int geo);
  * at the same floor (every query the first pass cuts is cut again: the floor-free third pass takes them).
  * All return the same candidates. */
 int fwav_debug_topk_floor(int mode, float value);
+/* Byte offsets of the fp16 search's workspace regions (K <= 64) for max_q queries over n_domains domains, as this
+ * library lays them out: offsets[0..14] = keys, share, ovf2, n_ovf2, seeds2, ovf1, n_ovf1, seeds1, miss, n_miss, miss2,
+ * n_miss2, floor_key, pilot, total (= fwav_sim_topk_workspace_size).  Every region before `pilot` sits at the same
+ * offset in libfwav.so; the product library adds the pilots' scores only where its floor can run. */
+int fwav_debug_sim_topk_layout(int64_t max_q, int64_t n_domains, int64_t* offsets);
 
 #ifdef __cplusplus
 }

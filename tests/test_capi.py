@@ -80,8 +80,8 @@ def test_every_knob_is_guarded():
         assert knobs and knobs <= named, (f, sorted(knobs - named))
 
 
-@pytest.mark.parametrize("switch", ["FWAV_TOPK_ABL=1", "FWAV_TOPK_EXTSEED", "FWAV_TOPK_DEBUG", "FWAV_TOPK_CENTSTATS",
-                                    "FWAV_TOPK_CENT_L2OFF", "FWAV_TOPK_G=2", "FWAV_TOPK_CB=4"])
+@pytest.mark.parametrize("switch", ["FWAV_TOPK_ABL=1", "FWAV_TOPK_CPMIN=4", "FWAV_TOPK_W=4", "FWAV_TOPK_G=2",
+                                    "FWAV_TOPK_CB=4"])
 def test_product_build_refuses_experiment_switches(switch):
     """An experiment code path compiled without -DFWAV_DEBUG_API stops the build (#error): the product library can
     carry none of them (libfwav_debug.so, built with -DFWAV_DEBUG_API, is where they compile)."""

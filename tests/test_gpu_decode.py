@@ -185,3 +185,39 @@ def test_early_exit_takes_reference_decision(side):
     outs = _shard_decode(idx, s, o, sym, pool, 8, dist.decode_bounds(nr, 3), kw["iterations"], eps, kw["s_damping"])
     assert bit_equal(np.concatenate([r.cpu().numpy() for r, _, _ in outs]), ref)
     assert all(r_ == it and dl[t] == dref[t] for _, r_, dl in outs)
+
+
+@pytest.mark.parametrize("side", ["stop", "go_on"])
+def test_decode_all_runs_to_the_reference_stop(side):
+    """fwav_decode_all (a C-ABI caller that never runs the check loop itself): one call resolves the exact
+    check and resumes on its own, with the oracle's iteration count, reconstruction and the reference's Δ at the
+    checked iteration — and without a check (default eps) it equals fwav_decode."""
+    from fwav import dist
+    from fwav._lib import call, size_call
+    idx, s, o, sym, pool = synth_matches(40_000, 6_000, 8, seed=77)
+    nr = len(idx)
+    base = dict(iterations=40, s_damping=0.5)
+    args = (idx, s, o, sym, pool, nr, 8)
+    _, _, d64 = O.decode(*args, convergence_eps=0.0, **base)
+    _, _, dref = O.decode(*args, convergence_eps=0.0, deltas="reference", **base)
+    beta = dist.decode_beta(nr * 8)
+    t = next(t for t in range(5, 40) if dref[t] != d64[t])
+    eps = dref[t] * (1 + beta / 4) if side == "stop" else dref[t] * (1 - beta / 4)
+    ref, it, _ = O.decode(*args, convergence_eps=eps, **base)
+    dev = torch.device("cuda", 0)
+    a = torch.empty(nr * 8, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    deltas = torch.zeros(40, dtype=torch.float64, device=dev)
+    state = torch.zeros(4, dtype=torch.int32, device=dev)
+    wsn = size_call("fwav_decode_all_workspace_size", nr, 8, 40)
+    ws = torch.empty(wsn, dtype=torch.uint8, device=dev)
+    ti, ts, to, tsym, tp = td(idx), td(s), td(o), td(sym), td(pool.reshape(-1))
+    call("fwav_decode_all", ti.data_ptr(), ts.data_ptr(), to.data_ptr(), tsym.data_ptr(), nr, 8, tp.data_ptr(),
+         len(pool), 40, eps, 16.0, 0.5, a.data_ptr(), b.data_ptr(), deltas.data_ptr(), state.data_ptr(),
+         ws.data_ptr(), wsn, torch.cuda.current_stream().cuda_stream)
+    st = state.cpu().numpy()
+    out = (b if st[2] == 1 else a).cpu().numpy()
+    # "go_on": the reference goes on at iteration t + 1 (the check) and stops later, or runs every iteration
+    assert st[1] == it and st[0] == (1 if it < 40 else 0), (st, it)
+    assert (it == t + 1) == (side == "stop")
+    assert bit_equal(out, ref) and deltas.cpu().numpy()[t] == dref[t]

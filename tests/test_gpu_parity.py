@@ -272,7 +272,7 @@ def test_overflow_with_sparse_active_list(first_mode):
     signal whose fp16 bands overflow must keep the overflow bookkeeping inside the workspace (guard bytes after it
     stay untouched) and return the all-f32 kernel's candidates."""
     from fwav import engine as E
-    from fwav._lib import size_call
+    from fwav._lib import sim_topk_layout, size_call
     sig = td(_periodic(192_000))  # ≈ 2,000 exact copies per query: > 192 even in each of 8 table pieces
     tile, K = 1024, 32
     rs, step = E.geometry(tile)
@@ -301,10 +301,8 @@ def test_overflow_with_sparse_active_list(first_mode):
         torch.cuda.synchronize()
         assert int(wsk[wsn:].count_nonzero().item()) == 0, "write past the workspace"
         out.append(cand.view(n, K)[rows.long()].cpu().numpy())
-        if e16 is not None:  # workspace tail: ovf list, its count, seeds — the exact-mode path must have run
-            # (after them: the floor's two miss lists + counts, two keys, the pilots' scores f32[1024·512·8 + 512])
-            floor_tail = 2 * 4 * (max_q + 1) + 8 + 4 * (1024 * 512 * 8 + 512)
-            o = wsn - floor_tail - 4 - 4 * max_q
+        if e16 is not None:  # the first pass's overflow count (the library's own layout): the exact path ran
+            o = sim_topk_layout(max_q, nd)["n_ovf1"]
             assert int(wsk[o:o + 4].view(torch.int32).item()) > 0
     assert np.array_equal(out[0], out[1])
 
