@@ -1965,10 +1965,11 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
 // k_merge_pieces' union: the pieces' bands hold n = Σ counts entries (cfg2: mean 174, max 268 over 60,416 queries;
 // those above the shared limit Lk mean 163; the band kept after the select mean 78, max 113: tools/diag/
 // merge_inputs.py, profiles/r06/merge_inputs_cfg2.log).  The entries above Lk are compacted into the wave's LDS row
-// and, up to kMergeFast·64 of them, selected from registers; a wider union (long runs of near-equal scores) is
+// and, up to merge_fast(MP)·64 of them, selected from registers; a wider union (long runs of near-equal scores) is
 // selected by re-reading it from L2 once per key bit instead, so the register budget — and the occupancy — no longer
 // scale with the widest plan's P·(C − 64).
-constexpr int kMergeFast = 8;
+// (The floor's second pass merges 16 pieces of a low floor: its unions above Lk run to ≈ 800 entries.)
+constexpr int merge_fast(int MP) { return MP <= 8 ? 8 : 16; }
 template <int C, int QB, bool HL, int MP>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
@@ -1982,7 +1983,7 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
   if (plan.R == 0 || plan.halves) return;
   const int lane = threadIdx.x & 63;
-  __shared__ uint64_t stage[4][kMergeFast * 64];  // per wave: the union above Lk, then the band (≤ C of it)
+  __shared__ uint64_t stage[4][merge_fast(MP) * 64];  // per wave: the union above Lk, then the band (≤ C of it)
   uint64_t* sw = stage[threadIdx.x >> 6];
   // one wave per split-block query.  (Persistent waves looping over the queries measured the same, cfg2 search 17.40
   // vs 17.39 ms, profiles/r05/ab_merge_persistent.log, but the loop made the compiler hoist per-lane invariants of
@@ -2005,6 +2006,7 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
                                             uint32_t fkey, const FloorCtl& fl) {
   constexpr int E = C / 64;
   constexpr int kBit0 = HL ? 0 : 12;  // the select's resolution (S16 needs the K-th only at ≈ 2^-11)
+  constexpr int kMergeFast = merge_fast(MP);
   const int64_t block = plan.F + w / QB;
   const int ql = (int)(w % QB);
   const int64_t qq = slot_query(block, ql, plan.nb, QB);

@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the timed steps (profiling passes)")
     ap.add_argument("--cpu-workers", default=None, help="CPU baseline search processes (default: sweep)")
+    ap.add_argument("--tie-order", default="numpy",
+                    help="compress_device tie_order (diagnostic: 'index' drops the host ranking of exactly tied rows, "
+                         "so matches may differ from the reference's where numpy's order among equal scores decides)")
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams that consecutive timed calls alternate over (a call's kernels stay on one); "
                          "the same default at every N, so that the driver's 1 -> N curve compares like with like")
@@ -248,7 +251,8 @@ def main():
             # the host half of numpy-order tie resolution (a few rows per step) overlaps the next step's search;
             # every step's outputs are final (wait()) before the timed region closes
             with torch.cuda.stream(call_stream()):
-                r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, events=ev, defer_ties=True)
+                r = engine.compress_device(sig, tile, K, energy_thresh=1e-4, events=ev, defer_ties=True,
+                                           tie_order=args.tie_order)
             step.pending.append(r)
             return r
     else:
@@ -256,7 +260,8 @@ def main():
 
         def step(ev=None, phases=False):
             def compute(s, t, k, thr, shard):
-                r = engine.compress_device(s, t, k, energy_thresh=thr, shard=shard, events=ev, defer_ties=not phases)
+                r = engine.compress_device(s, t, k, energy_thresh=thr, shard=shard, events=ev, defer_ties=not phases,
+                                           tie_order=args.tie_order)
                 step.last = r
                 step.sig_local = s
                 return None if r.empty else dict(idx=r.idx, s=r.s, o=r.o, sym=r.sym, err=r.err, pool=r.pool,
@@ -368,7 +373,8 @@ def main():
         "metric": "ranges matched/sec at tile_size=2048, top-K=64",
         "value": value, "unit": "ranges/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-        "dtype": "f32", "data": f"synthetic ({args.config} generator, seed 0; one signal, ranges sharded over ranks)",
+        "dtype": "f32", "data": f"synthetic ({args.config} generator, seed 0; one signal, ranges sharded over ranks)"
+                                + ("" if args.tie_order == "numpy" else f"; tie_order={args.tie_order} (diagnostic)"),
         "config": {"workload": f"{args.config}: {sig_h.size / sr:.0f} s {sr} Hz "
                                f"{WORKLOAD_TEXT.get(args.config, '').split(' ', 4)[-1]}, tile_size={tile}, "
                                f"top_k={K}, n_ranges={nr}, n_domains={nd}",
