@@ -553,10 +553,14 @@ struct TopkPlan {
 // seed; a query whose exact K-th score does not clear f + δ (δ ≥ |s16 − s32|, ≥ |shl − s32|: when it does, every exact
 // top-K member had a filter score above f, and the result is exact) is listed in miss[0 .. *n_miss) for the
 // floor-free second pass instead of being emitted.
+// alt_rt / alt_p: the work plan when *key is 0 — the floor did not apply (fewer active queries on the device than the
+// floor's minimum, or no finite pilot estimate): the launch then runs the plan of a floor-free pass (its grid covers
+// both plans), not the floor's fewer, longer table pieces.
 struct FloorCtl {
   const uint32_t* key;
   int32_t* miss;
   int32_t* n_miss;
+  int alt_rt = -1, alt_p = 1;
 };
 // Whole wave: true (and the query listed for the second pass) when the floor may have cut a member of its top K:
 // fewer than K band entries, or a K-th exact score (kth: key) not above f + δ.  Every domain whose filter score
@@ -1503,7 +1507,10 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
 
   const int n_active = *n_active_p;
   constexpr int QB = 32 * NG;  // queries per block
-  const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
+  // a first pass's speculative floor (FloorCtl): every band limit starts there; none applied → the floor-free plan
+  const uint32_t fkey = (!EX && fl.key != nullptr) ? __builtin_amdgcn_readfirstlane(*fl.key) : 0u;
+  const bool alt = fl.key != nullptr && fkey == 0u;
+  const TopkPlan plan = make_plan(n_active, alt ? fl.alt_rt : plan_rt, alt ? fl.alt_p : plan_p, QB);
   int64_t block;
   int piece, npieces, qhalf;
   plan_item(plan, blockIdx.x, block, piece, npieces, qhalf);
@@ -1588,8 +1595,6 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     for (int s = 0; s < QS; ++s)
       if (upd[s]) thf[s] = fmaxf(thf[s], inseed[s]);
   }
-  // a first pass's speculative floor (FloorCtl): every band limit starts there
-  const uint32_t fkey = (!EX && fl.key != nullptr) ? __builtin_amdgcn_readfirstlane(*fl.key) : 0u;
   if (fkey != 0u) {
 #pragma unroll
     for (int s = 0; s < QS; ++s)
@@ -1980,7 +1985,8 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
                                                       int32_t* __restrict__ ties, FloorCtl fl) {
   const int n_active = *n_active_p;
   const uint32_t fkey = fl.key != nullptr ? __builtin_amdgcn_readfirstlane(*fl.key) : 0u;
-  const TopkPlan plan = make_plan(n_active, plan_rt, plan_p, QB);
+  const bool alt = fl.key != nullptr && fkey == 0u;  // the floor did not apply: the floor-free plan (FloorCtl)
+  const TopkPlan plan = make_plan(n_active, alt ? fl.alt_rt : plan_rt, alt ? fl.alt_p : plan_p, QB);
   if (plan.R == 0 || plan.halves) return;
   const int lane = threadIdx.x & 63;
   __shared__ uint64_t stage[4][merge_fast(MP) * 64];  // per wave: the union above Lk, then the band (≤ C of it)
@@ -2608,9 +2614,18 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     float* pilot = reinterpret_cast<float*>(wb + lay.pilot);
     // One first pass (search + merge of split blocks) over act[0 .. *nact) in geometry g with plan (rt, P) and floor
     // fl; `diag`: the debug library's counter / ablation launches may replace the search
+    // (with a floor the device runs the floor-free plan fl.alt_* when the floor did not apply: the grid, the shared
+    // limits and the merge cover both plans)
     auto first_pass = [&](const int32_t* act, const int32_t* nact, int g, int rt, int P, FloorCtl fl, bool diag) {
-      const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(g));
-      if (pl.R > 0 && !pl.halves) (void)hipMemsetAsync(share, 0, (size_t)q1 * sizeof(uint32_t), st);
+      const TopkPlan pl0 = make_plan(max_q, rt, P, geometry_qb(g));
+      const TopkPlan pla = fl.key != nullptr ? make_plan(max_q, fl.alt_rt, fl.alt_p, geometry_qb(g)) : pl0;
+      struct {
+        int64_t n, R;
+        int P;
+        int64_t items() const { return n; }
+      } pl{std::max(pl0.items(), pla.items()), std::max(pl0.R, pla.R), std::max(pl0.P, pla.P)};
+      if ((pl0.R > 0 && !pl0.halves) || (pla.R > 0 && !pla.halves))
+        (void)hipMemsetAsync(share, 0, (size_t)q1 * sizeof(uint32_t), st);
 #define FWAV_FIRST(MODE_, STATS_, DBG_, ST_)                                                                    \
   k_sim_topk_f16<k16Cap, STATS_, MODE_><<<pl.items(), 64 * k16Waves, 0, st>>>(                                  \
       emb16, emb, nd, act, nact, q_offset, K, cand, gkeys, ovf1, n_ovf1, share, nullptr, 0.0f, rt, P, DBG_, ST_,  \
@@ -2700,13 +2715,15 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
         k_floor_reduce<<<1, kFloorPilots, 0, st>>>(est, g_floor_rank, n_active, fmode == 2 ? 0 : (int)kFloorMinQ,
                                                    floor_key);
       }
-      fl = FloorCtl{floor_key, miss, n_miss};
+      int rt_nf, P_nf;  // the plan when the device finds the floor does not apply
+      host_plan_for(max_q, nd, geo, rt_nf, P_nf, 0);
+      fl = FloorCtl{floor_key, miss, n_miss, rt_nf, P_nf};
     }
     first_pass(active, n_active, geo, rt, P, fl, true);
     if (use_floor) {
       int rt2, P2;
       floor_plan(max_q, nd, rt2, P2);
-      first_pass(miss, n_miss, kGeoBase, rt2, P2, FloorCtl{floor_key + 1, miss2, n_miss2}, false);
+      first_pass(miss, n_miss, kGeoBase, rt2, P2, FloorCtl{floor_key + 1, miss2, n_miss2, rt2, P2}, false);
       first_pass(miss2, n_miss2, kGeoBase, rt2, P2, FloorCtl{nullptr, nullptr, nullptr}, false);
     }
     // Queries whose band overflowed the buffer (large groups of equal or nearly equal scores) are searched again by
