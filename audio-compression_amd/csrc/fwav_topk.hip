@@ -1959,7 +1959,7 @@ __device__ __forceinline__ void merge_band(const uint64_t* __restrict__ sw, int 
 
 // One split-block query of k_merge_pieces (defined below the kernel); MP ≥ the plan's pieces.
 template <int C, int QB, bool HL, int MP>
-__device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int lane, uint64_t* sw,
+__device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int lane, uint64_t* sw, uint32_t* sh,
                                             const uint64_t* __restrict__ gkeys_all, const int32_t* __restrict__ active,
                                             int n_active, int K, int32_t* __restrict__ cand,
                                             int32_t* __restrict__ ovf_list, int32_t* __restrict__ n_ovf,
@@ -1973,8 +1973,10 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
 // and, up to merge_fast(MP)·64 of them, selected from registers; a wider union (long runs of near-equal scores) is
 // selected by re-reading it from L2 once per key bit instead, so the register budget — and the occupancy — no longer
 // scale with the widest plan's P·(C − 64).
-// (The floor's second pass merges 16 pieces of a low floor: its unions above Lk run to ≈ 800 entries.)
-constexpr int merge_fast(int MP) { return MP <= 8 ? 8 : 16; }
+// (The floor's second pass merges 16 or 32 pieces of a low floor: its unions above Lk run to ≈ 800 entries and more;
+// there the union's key words, merge_hi_rows(MP) rows of them, are selected from LDS before the L2 tier.)
+constexpr int kMergeFast = 8;
+constexpr int merge_hi_rows(int MP) { return MP <= 8 ? 1 : 32; }
 template <int C, int QB, bool HL, int MP>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
@@ -1989,21 +1991,23 @@ __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict
   const TopkPlan plan = make_plan(n_active, alt ? fl.alt_rt : plan_rt, alt ? fl.alt_p : plan_p, QB);
   if (plan.R == 0 || plan.halves) return;
   const int lane = threadIdx.x & 63;
-  __shared__ uint64_t stage[4][merge_fast(MP) * 64];  // per wave: the union above Lk, then the band (≤ C of it)
+  __shared__ uint64_t stage[4][kMergeFast * 64];  // per wave: the union above Lk, then the band (≤ C of it)
+  __shared__ uint32_t hstage[4][merge_hi_rows(MP) * 64];  // per wave (16 / 32 pieces): the union's key words
   uint64_t* sw = stage[threadIdx.x >> 6];
+  uint32_t* sh = hstage[threadIdx.x >> 6];
   // one wave per split-block query.  (Persistent waves looping over the queries measured the same, cfg2 search 17.40
   // vs 17.39 ms, profiles/r05/ab_merge_persistent.log, but the loop made the compiler hoist per-lane invariants of
   // the body out of it: 131 VGPRs, 3 waves per SIMD.)
   // (wave-uniform values in scalar registers: the query's row, limit and addresses load through the scalar cache)
   const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (w < plan.R * QB)
-    merge_query<C, QB, HL, MP>(plan, w, lane, sw, gkeys_all, active, n_active, K, cand, ovf_list, n_ovf, share, emb,
-                               q_offset, sp, ties, fkey, fl);
+    merge_query<C, QB, HL, MP>(plan, w, lane, sw, sh, gkeys_all, active, n_active, K, cand, ovf_list, n_ovf, share,
+                               emb, q_offset, sp, ties, fkey, fl);
 }
 
 // One split-block query w of k_merge_pieces (whole wave; sw: the wave's LDS row).
 template <int C, int QB, bool HL, int MP>
-__device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int lane, uint64_t* sw,
+__device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int lane, uint64_t* sw, uint32_t* sh,
                                             const uint64_t* __restrict__ gkeys_all, const int32_t* __restrict__ active,
                                             int n_active, int K, int32_t* __restrict__ cand,
                                             int32_t* __restrict__ ovf_list, int32_t* __restrict__ n_ovf,
@@ -2012,7 +2016,7 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
                                             uint32_t fkey, const FloorCtl& fl) {
   constexpr int E = C / 64;
   constexpr int kBit0 = HL ? 0 : 12;  // the select's resolution (S16 needs the K-th only at ≈ 2^-11)
-  constexpr int kMergeFast = merge_fast(MP);
+  constexpr int kHiRows = merge_hi_rows(MP);
   const int64_t block = plan.F + w / QB;
   const int ql = (int)(w % QB);
   const int64_t qq = slot_query(block, ql, plan.nb, QB);
@@ -2068,6 +2072,7 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
         const int pos = m + __popcll(bm & ((1ull << lane) - 1ull));
         if (in) {
           if (pos < kMergeFast * 64) sw[pos] = y[i];
+          if (kHiRows > 1 && pos < kHiRows * 64) sh[pos] = (uint32_t)(y[i] >> 32);
           a &= (uint32_t)(y[i] >> 32);
           o |= (uint32_t)(y[i] >> 32);
         }
@@ -2107,6 +2112,32 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
           const uint64_t bm = __ballot(keep);
           const int pos = mb + __popcll(bm & ((1ull << lane) - 1ull));
           if (keep && pos < C) sw[pos] = x[u];
+          mb += __popcll(bm);
+        }
+      }
+    } else if (kHiRows > 1 && m <= kHiRows * 64) {
+      // a wider union (16 / 32 pieces): the select over its key words in LDS, then the band re-streamed from L2
+      if (m > K) {
+#pragma unroll 1
+        for (int bit = top; bit >= kBit0; --bit) {
+          const uint32_t Tc = T | (1u << bit);
+          int c = 0;
+#pragma unroll 1
+          for (int u = 0; u < mu; ++u) c += __popcll(__ballot(u * 64 + lane < m && sh[u * 64 + lane] >= Tc));
+          if (c >= K) T = Tc;
+        }
+        L = max(L, f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta));
+      }
+      for (int u0 = 0; u0 < nu; u0 += kMergeFast) {
+        uint64_t y[kMergeFast];
+#pragma unroll
+        for (int i = 0; i < kMergeFast; ++i) y[i] = u0 + i < nu ? entry((u0 + i) * 64 + lane) : 0ull;
+#pragma unroll
+        for (int i = 0; i < kMergeFast; ++i) {
+          const bool keep = (uint32_t)(y[i] >> 32) > L;
+          const uint64_t bm = __ballot(keep);
+          const int pos = mb + __popcll(bm & ((1ull << lane) - 1ull));
+          if (keep && pos < C) sw[pos] = y[i];
           mb += __popcll(bm);
         }
       }
@@ -2331,9 +2362,12 @@ constexpr int64_t kFloorMinQ = 65536, kFloorMinD = 65536;
 // 86.4 M domains the second pass took 204 ms after a 511 ms first pass (a 262,144-query search, profiles/r05/
 // kernel_stats_bench_cfg2.txt: the cfg4 affine-roofline extra of bench.py)
 constexpr int64_t kFloorMaxD = int64_t(1) << 22;
-constexpr int kFloorP2 = 16;  // the second pass's table pieces per split block
+// the second pass's table pieces per split block: 32 where the misses expected at the floor's rank (≈ 2 % of the
+// launch) fill at most one round of workgroup slots in 32 pieces (the pass's latency is the length of one piece:
+// 82,688 queries 4.86 → 4.60 ms with the round's faster pilots and merge, profiles/r06/ab_floor_p2_quarter.log), else
+// 16 (cfg2's ≈ 5,000 misses in 21 blocks × 16 pieces fill one round; 32 pieces would take two)
+constexpr int kFloorP2 = 16, kFloorP2Few = 32;
 constexpr int kFloorPilots = 512;  // pilot queries (evenly spaced over the active list)
-constexpr int kFloorWG = 1024;     // k_floor_pilot workgroups, each over a 1/kFloorWG slice of the sampled domains
 constexpr int kFloorJ = 8;         // the pilot's estimate: its j-th best score over every (K/j)-th domain ≈ its K-th
 constexpr int kFloorRank = 10;    // the floor: the pilots' kFloorRank-th smallest estimate (≈ their 2 % quantile)
 // second pass: up to kFloorSplit blocks (of 256 misses) split into kFloorP2 pieces, any further ones
@@ -2346,7 +2380,7 @@ constexpr int kFloorSplit = 64;
 // pieces do not start cold either; the queries that one cuts (normally none) take a floor-free third pass.  (Full
 // score rows for them, launch_topk_large, measured 3.6 ms per launch: one workgroup per row streams it repeatedly.)
 constexpr float kFloor2Margin = 0.15f;
-static_assert(kFloorP2 >= 1 && kFloorP2 <= kMaxPieces, "second-pass pieces outside the merge");
+static_assert(kFloorP2 >= 1 && kFloorP2Few <= kMaxPieces, "second-pass pieces outside the merge");
 #ifdef FWAV_DEBUG_API
 static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 / 3 forced value, 2 pilot at any size
 static uint32_t g_floor_key = 0u;
@@ -2363,39 +2397,57 @@ static bool floor_by_default(int64_t max_q, int64_t nd) {
   return fmode != 0 && (fmode > 0 || (max_q >= kFloorMinQ && nd >= kFloorMinD && nd <= kFloorMaxD));
 }
 // second-pass plan (base geometry) for a miss list of at most max_q queries: every piece streams ≥ 16 chunks
+#ifdef FWAV_DEBUG_API
+static int g_floor_p2 = 0;  // fwav_debug_topk_floor_pieces (debug library only; 0: by the launch's size)
+#else
+constexpr int g_floor_p2 = 0;
+#endif
 static void floor_plan(int64_t max_q, int64_t nd, int& rt, int& P) {
-  (void)max_q;
   rt = kFloorSplit;
   const int64_t pmax = cdiv(nd, kChunk) / 16;
-  P = (int)std::max<int64_t>(1, std::min<int64_t>(kFloorP2, pmax));
+  int cus, per_cu;
+  topk_device_slots(kGeoBase, cus, per_cu);
+  const int64_t blocks = cdiv(cdiv(max_q > 0 ? max_q : 1, 50), k16QB);  // ≈ 2 % of the launch, in 256-query blocks
+  const int p2 = g_floor_p2 > 0 ? g_floor_p2 : (blocks * kFloorP2Few <= (int64_t)cus * per_cu ? kFloorP2Few : kFloorP2);
+  P = (int)std::max<int64_t>(1, std::min<int64_t>(p2, pmax));
 }
 
-// Each pilot p (of kFloorPilots, 2 per thread) at active position p·n/kFloorPilots: its kFloorJ best f32 scores over
-// the sampled domains m·stride of this workgroup's slice, to scratch[(p·gridDim + block)·kFloorJ + i].  The slice's
-// domain rows are staged in LDS 256 at a time.  (A guess only: no reference order needed.)
+// The pilots' sampled scores: workgroup (g, s) = (blockIdx.x % kPilotGroups, blockIdx.x / kPilotGroups) scores the 64
+// pilots g·64 + lane (pilot p at active position p·n/kFloorPilots) against slice s of the sampled domains m·stride
+// (1/kFloorSlices of them; its rows staged in LDS 256 at a time, every 4th row to each of the 4 waves), keeps each
+// pilot's kFloorJ best per wave, merges the 4 waves' lists in LDS and writes them to scratch[(p·kFloorSlices + s)·kFloorJ
+// + i] (pilot-major: k_floor_est reads a pilot's entries contiguously).  The dot products in packed f32 FMAs (a guess
+// only: no reference order needed).  Round 5 put 2 pilots on each thread of 1,024 one-dimensional slices and wrote
+// 16 MB of pilot-major entries in 32-B pieces 32 KB apart: 136 µs, plus 47 µs in k_floor_est.
+constexpr int kPilotGroups = kFloorPilots / 64, kFloorSlices = 128;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void k_floor_pilot(const float* __restrict__ emb, int64_t nd,
                                                      const int32_t* __restrict__ active,
                                                      const int32_t* __restrict__ n_active_p, int64_t q_offset,
                                                      int stride, float* __restrict__ scratch) {
   __shared__ float4 rows[256][4];
+  __shared__ float lists[4][64][kFloorJ + 1];
   const int na = *n_active_p;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = blockIdx.x % kPilotGroups, sl = blockIdx.x / kPilotGroups;
+  const int p = g * 64 + lane;
   const int64_t M = (nd + stride - 1) / stride;
-  const int64_t m0 = M * blockIdx.x / gridDim.x, m1 = M * (blockIdx.x + 1) / gridDim.x;
-  float q[2][16], top[2][kFloorJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int p = threadIdx.x * 2 + i;
+  const int64_t m0 = M * sl / kFloorSlices, m1 = M * (sl + 1) / kFloorSlices;
+  f32x2 q[8];
+  {
     const int64_t pos = na > 0 ? (int64_t)p * na / kFloorPilots : 0;
     const int64_t row = na > 0 ? (int64_t)active[pos] + q_offset : 0;
     const float4* qp = reinterpret_cast<const float4*>(emb + row * 16);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float4 v = qp[k];
-      q[i][4 * k] = v.x; q[i][4 * k + 1] = v.y; q[i][4 * k + 2] = v.z; q[i][4 * k + 3] = v.w;
+      q[2 * k] = f32x2{v.x, v.y};
+      q[2 * k + 1] = f32x2{v.z, v.w};
     }
-#pragma unroll
-    for (int k = 0; k < kFloorJ; ++k) top[i][k] = -INFINITY;
   }
+  float top[kFloorJ];
+#pragma unroll
+  for (int k = 0; k < kFloorJ; ++k) top[k] = -INFINITY;
   for (int64_t mb = m0; mb < m1; mb += 256) {
     const int nr = (int)min<int64_t>(256, m1 - mb);
     __syncthreads();
@@ -2405,38 +2457,50 @@ __global__ __launch_bounds__(256) void k_floor_pilot(const float* __restrict__ e
       for (int k = 0; k < 4; ++k) rows[threadIdx.x][k] = rp[k];
     }
     __syncthreads();
-    for (int r = 0; r < nr; ++r) {
-      float4 d[4];
+    for (int r = wave; r < nr; r += 4) {
+      f32x2 acc = f32x2{0.0f, 0.0f};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) d[k] = rows[r][k];
+      for (int k = 0; k < 4; ++k) {
+        const float4 d = rows[r][k];
+        acc = __builtin_elementwise_fma(q[2 * k], f32x2{d.x, d.y}, acc);
+        acc = __builtin_elementwise_fma(q[2 * k + 1], f32x2{d.z, d.w}, acc);
+      }
+      float x = acc.x + acc.y;
+      // sorted insertion into the pilot's top kFloorJ (descending), only for a score that enters it
+      if (x > top[kFloorJ - 1]) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        // two independent partial sums (a shorter dependent chain)
-        float x0 = 0.0f, x1 = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          x0 += q[i][4 * k] * d[k].x + q[i][4 * k + 1] * d[k].y + q[i][4 * k + 2] * d[k].z + q[i][4 * k + 3] * d[k].w;
-          x1 += q[i][8 + 4 * k] * d[2 + k].x + q[i][9 + 4 * k] * d[2 + k].y + q[i][10 + 4 * k] * d[2 + k].z +
-                q[i][11 + 4 * k] * d[2 + k].w;
-        }
-        float x = x0 + x1;
-        // sorted insertion into the pilot's top kFloorJ (descending), only for a score that enters it
-        if (x > top[i][kFloorJ - 1]) {
-#pragma unroll
-          for (int k = 0; k < kFloorJ; ++k) {
-            const float hi = fmaxf(top[i][k], x);
-            x = fminf(top[i][k], x);
-            top[i][k] = hi;
-          }
+        for (int k = 0; k < kFloorJ; ++k) {
+          const float hi = fmaxf(top[k], x);
+          x = fminf(top[k], x);
+          top[k] = hi;
         }
       }
     }
   }
+  // the 4 waves' lists of each pilot merged by wave 0
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int k = 0; k < kFloorJ; ++k) lists[wave][lane][k] = top[k];
+  __syncthreads();
+  if (wave == 0) {
 #pragma unroll
-    for (int k = 0; k < kFloorJ; ++k)
-      scratch[((int64_t)(threadIdx.x * 2 + i) * gridDim.x + blockIdx.x) * kFloorJ + k] = top[i][k];
+    for (int w = 1; w < 4; ++w)
+#pragma unroll
+      for (int i = 0; i < kFloorJ; ++i) {
+        float x = lists[w][lane][i];
+        if (x > top[kFloorJ - 1]) {
+#pragma unroll
+          for (int k = 0; k < kFloorJ; ++k) {
+            const float hi = fmaxf(top[k], x);
+            x = fminf(top[k], x);
+            top[k] = hi;
+          }
+        }
+      }
+    float4* out = reinterpret_cast<float4*>(scratch + ((int64_t)p * kFloorSlices + sl) * kFloorJ);
+    static_assert(kFloorJ == 8, "two float4 per list");
+    out[0] = make_float4(top[0], top[1], top[2], top[3]);
+    out[1] = make_float4(top[4], top[5], top[6], top[7]);
+  }
 }
 
 // One wave per pilot (block = pilot): its j-th best score over all nwg slices (its estimate of its K-th score), to
@@ -2535,7 +2599,7 @@ struct TopkLayout {
   size_t keys, share, ovf2, n_ovf2, seeds2, ovf1, n_ovf1, seeds1, miss, n_miss, miss2, n_miss2, floor_key, pilot,
       total;
 };
-constexpr size_t kPilotBytes = ((size_t)kFloorWG * kFloorPilots * kFloorJ + kFloorPilots) * sizeof(float);
+constexpr size_t kPilotBytes = ((size_t)kFloorPilots * kFloorSlices * kFloorJ + kFloorPilots) * sizeof(float);
 static TopkLayout topk_layout(int64_t max_q, int64_t nd) {
   const size_t q = (size_t)(max_q > 0 ? max_q : 1);
   TopkLayout L;
@@ -2709,9 +2773,9 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
         (void)hipMemsetD32Async((hipDeviceptr_t)(floor_key + 1), fmode == 3 ? (int)g_floor_key : 0, 1, st);
       } else {
         const int j = K < kFloorJ ? K : kFloorJ, stride = K / j;
-        float* est = pilot + (size_t)kFloorWG * kFloorPilots * kFloorJ;
-        k_floor_pilot<<<kFloorWG, 256, 0, st>>>(emb, nd, active, n_active, q_offset, stride, pilot);
-        k_floor_est<<<kFloorPilots, 64, 0, st>>>(pilot, kFloorWG, j, est);
+        float* est = pilot + (size_t)kFloorPilots * kFloorSlices * kFloorJ;
+        k_floor_pilot<<<kPilotGroups * kFloorSlices, 256, 0, st>>>(emb, nd, active, n_active, q_offset, stride, pilot);
+        k_floor_est<<<kFloorPilots, 64, 0, st>>>(pilot, kFloorSlices, j, est);
         k_floor_reduce<<<1, kFloorPilots, 0, st>>>(est, g_floor_rank, n_active, fmode == 2 ? 0 : (int)kFloorMinQ,
                                                    floor_key);
       }
@@ -2873,6 +2937,14 @@ int fwav_debug_topk_floor(int mode, float value) {
   uint32_t u;
   std::memcpy(&u, &value, sizeof u);
   g_floor_key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // f2key
+  return FWAV_OK;
+}
+
+// Diagnostic override of the floor's second-pass table pieces per split block (1 … 32; 0: by the launch's size, the
+// default).  Re-query fwav_sim_topk_workspace_size afterwards.
+int fwav_debug_topk_floor_pieces(int p2) {
+  FWAV_CHECK_ARG(p2 >= 0 && p2 <= kMaxPieces, FWAV_ERR_ARG, "fwav_debug_topk_floor_pieces: outside [0, %d]", kMaxPieces);
+  g_floor_p2 = p2;
   return FWAV_OK;
 }
 

@@ -77,6 +77,7 @@ DEBUG_SIGNATURES = {
     "fwav_debug_topk_plan_info": (I32, [I64, I64, P, P]),
     "fwav_debug_topk_qb": (I64, [I32]),
     "fwav_debug_topk_floor": (I32, [I32, F32]),
+    "fwav_debug_topk_floor_pieces": (I32, [I32]),
     "fwav_debug_sim_topk_layout": (I32, [I64, I64, P]),
 }
 
@@ -144,6 +145,8 @@ def debug_lib() -> C.CDLL:
             _libs["debug"].fwav_debug_topk_floor(int(mode), float(value or 0.0))
         if os.environ.get("FWAV_DEBUG_TOPK_GEOMETRY"):
             _libs["debug"].fwav_debug_topk_geometry(int(os.environ["FWAV_DEBUG_TOPK_GEOMETRY"]))
+        if os.environ.get("FWAV_DEBUG_TOPK_P2"):
+            _libs["debug"].fwav_debug_topk_floor_pieces(int(os.environ["FWAV_DEBUG_TOPK_P2"]))
     return _libs["debug"]
 
 
@@ -173,6 +176,7 @@ class debug_library:
         d.fwav_debug_topk_mode(-1)
         d.fwav_debug_topk_geometry(-1)
         d.fwav_debug_topk_floor(-1, 0.0)
+        d.fwav_debug_topk_floor_pieces(0)
         _active = self.prev
         return False
 

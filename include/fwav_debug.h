@@ -56,6 +56,10 @@ int64_t fwav_debug_topk_qb(int geo);
  * at the same floor (every query the first pass cuts is cut again: the floor-free third pass takes them).
  * All return the same candidates. */
 int fwav_debug_topk_floor(int mode, float value);
+/* Diagnostic override of the floor's second pass: table pieces per split block of misses (1 … 32; 0 = the default:
+ * 32 below 131,072 queries, else 16).  Re-query fwav_sim_topk_workspace_size afterwards.  All return the same
+ * candidates. */
+int fwav_debug_topk_floor_pieces(int pieces);
 /* Byte offsets of the fp16 search's workspace regions (K <= 64) for max_q queries over n_domains domains, as this
  * library lays them out: offsets[0..14] = keys, share, ovf2, n_ovf2, seeds2, ovf1, n_ovf1, seeds1, miss, n_miss, miss2,
  * n_miss2, floor_key, pilot, total (= fwav_sim_topk_workspace_size).  Every region before `pilot` sits at the same
