@@ -521,7 +521,7 @@ constexpr int k16QB = 32 * k16Waves * k16Sets;  // queries per block (one workgr
 // a first pass's table pieces per split block (merge: P·(C − 64) keys per query at most) ...
 constexpr int kPlanMaxPieces = FWAV_TOPK_MAXP;
 // ... and any plan's, the floor's later passes included (k_merge_pieces is instantiated for ≤ 8, 16 and 32 pieces)
-constexpr int kMaxPieces = 32;
+constexpr int kMaxPieces = 64;
 static_assert(kPlanMaxPieces <= kMaxPieces, "first-pass plans stay within the merge's widest instantiation");
 
 // Work plan of the fp16 search.  The n_blocks query blocks are items of one launch, dispatched in order: the first
@@ -2237,7 +2237,12 @@ constexpr int kCentFloorPieces = 3;  // ... and this many with the speculative f
 #define FWAV_TOPK_CENT_HL 0  // the centroid geometry for hi/lo first passes too (cfg3: 195 vs 180 ms base)
 #endif
 #ifndef FWAV_TOPK_CENT_MINQ
-#define FWAV_TOPK_CENT_MINQ 60000  // the centroid geometry for first passes of at least this many queries
+// the centroid geometry for first passes of at least this many queries.  Below the speculative floor's minimum the
+// centroid geometry lost to the base one (cold limits: 41,344 queries 3.42 vs 3.26 ms); with the floor it wins from
+// 32,768 queries on (round 6, tools/ab/eighth_geo_prof.sh, profiles/r06/eighth_geo_*.log, floor on / base geometry,
+// floor off, base geometry → floor on, centroid: 32,768 queries 2.73 / 2.80 → 2.42 ms, 41,344 2.93 / 3.22 → 2.88,
+// 55,000 4.38 / 4.35 → 3.75), not at 20,672 (2.12 / 2.07 → 2.36: 41 blocks of 512 fill 328 of the 512 slots)
+#define FWAV_TOPK_CENT_MINQ 32768
 #endif
 static int first_geometry(int64_t nd, int64_t max_q) {
   if (g_wide >= 0) return g_wide;
@@ -2356,8 +2361,9 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P, i
 // The later passes cost a round of table pieces whatever their size (≈ 0.5–1 ms: a piece's cost is mostly the rise
 // of its limit), so the floor pays only where it saves more than that (tools/floor_pass_ab.py, pilots' 10th-smallest
 // estimate, same box): 330,750 queries 18.15 → 15.90 ms, 165,375 9.70 → 8.65, 82,688 6.14 → 5.33, but 41,344 (one
-// rank's share at N = 8) 3.40 → 3.94 (profiles/r05/floor_pass_ab.log, floor_pass_ab_mid.log)
-constexpr int64_t kFloorMinQ = 65536, kFloorMinD = 65536;
+// rank's share at N = 8) 3.40 → 3.94 (profiles/r05/floor_pass_ab.log, floor_pass_ab_mid.log) — in the base
+// geometry; with the centroid geometry the floor pays from 32,768 queries on (round 6, FWAV_TOPK_CENT_MINQ)
+constexpr int64_t kFloorMinQ = 32768, kFloorMinD = 65536;
 // ... and tables of at most kFloorMaxD domains: the later passes' pieces grow with the table, and at cfg4's
 // 86.4 M domains the second pass took 204 ms after a 511 ms first pass (a 262,144-query search, profiles/r05/
 // kernel_stats_bench_cfg2.txt: the cfg4 affine-roofline extra of bench.py)
@@ -2385,10 +2391,12 @@ static_assert(kFloorP2 >= 1 && kFloorP2Few <= kMaxPieces, "second-pass pieces ou
 static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 / 3 forced value, 2 pilot at any size
 static uint32_t g_floor_key = 0u;
 static int g_floor_rank = kFloorRank;
+static float g_floor2_margin = kFloor2Margin;
 #else
 constexpr int g_floor_mode = -1;
 constexpr uint32_t g_floor_key = 0u;
 constexpr int g_floor_rank = kFloorRank;
+constexpr float g_floor2_margin = kFloor2Margin;
 #endif
 static int floor_mode() { return g_floor_mode; }
 // the first pass of max_q queries over nd domains runs with the floor (K ≤ 64, the fp16 search)
@@ -2543,7 +2551,7 @@ __global__ __launch_bounds__(64) void k_floor_est(const float* __restrict__ scra
 // active queries, or no finite estimate) and the smallest − kFloor2Margin for the second pass.
 __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __restrict__ est_g, int rank,
                                                                const int32_t* __restrict__ n_active_p, int min_q,
-                                                               uint32_t* __restrict__ floor_key) {
+                                                               float margin2, uint32_t* __restrict__ floor_key) {
   __shared__ float est[kFloorPilots];
   const int p = threadIdx.x;
   // a NaN estimate ranks as +inf (after every number), so each place 0 … kFloorPilots − 1 has exactly one owner and
@@ -2562,7 +2570,7 @@ __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __re
   const int na = *n_active_p;
   const bool ok = na >= min_q && na > 0 && e > -INFINITY && e < INFINITY;
   if (place == rank - 1) floor_key[0] = ok ? f2key(e) : 0u;
-  if (place == 0) floor_key[1] = ok ? f2key(e - kFloor2Margin) : 0u;
+  if (place == 0) floor_key[1] = ok ? f2key(e - margin2) : 0u;
 }
 
 // Key-buffer bytes: enough for the first pass in either geometry (a diagnostic override may switch it between the
@@ -2742,6 +2750,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
   do {                                                                                                          \
     if (pl.P <= 8) FWAV_MERGE_MP(QB_, HL_, 8);                                                                  \
     else if (pl.P <= 16) FWAV_MERGE_MP(QB_, HL_, 16);                                                           \
+    else if (pl.P <= 32) FWAV_MERGE_MP(QB_, HL_, 32);                                                           \
     else FWAV_MERGE_MP(QB_, HL_, kMaxPieces);                                                                   \
   } while (0)
         if (g == kGeoWide) {
@@ -2761,7 +2770,8 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     // (K/8)-th domain (k_floor_pilot), a guess at the lowest K-th score of the search; the queries it may cut are
     // searched again at a lower floor, and the few that one cuts without any (base geometry, table pieces).
     const int fmode = floor_mode();
-    const bool use_floor = !stats_first && K <= 64 && floor_by_default(max_q, nd);
+    // (counter launches run without the floor unless dbg bit 19 asks for the product's floor too)
+    const bool use_floor = (!stats_first || (dbg & (1 << 19))) && K <= 64 && floor_by_default(max_q, nd);
     int rt, P;
     host_plan_for(max_q, nd, geo, rt, P, use_floor ? 1 : 0);
     FloorCtl fl{nullptr, nullptr, nullptr};
@@ -2777,7 +2787,7 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
         k_floor_pilot<<<kPilotGroups * kFloorSlices, 256, 0, st>>>(emb, nd, active, n_active, q_offset, stride, pilot);
         k_floor_est<<<kFloorPilots, 64, 0, st>>>(pilot, kFloorSlices, j, est);
         k_floor_reduce<<<1, kFloorPilots, 0, st>>>(est, g_floor_rank, n_active, fmode == 2 ? 0 : (int)kFloorMinQ,
-                                                   floor_key);
+                                                   g_floor2_margin, floor_key);
       }
       int rt_nf, P_nf;  // the plan when the device finds the floor does not apply
       host_plan_for(max_q, nd, geo, rt_nf, P_nf, 0);
@@ -2929,10 +2939,13 @@ int fwav_debug_topk_geometry(int wide) {
 
 // Diagnostic override of the speculative floor (include/fwav_debug.h).
 int fwav_debug_topk_floor(int mode, float value) {
-  FWAV_CHECK_ARG(mode >= -1 && mode <= 3, FWAV_ERR_ARG, "fwav_debug_topk_floor: mode outside [-1, 3]");
+  FWAV_CHECK_ARG(mode >= -1 && mode <= 4, FWAV_ERR_ARG, "fwav_debug_topk_floor: mode outside [-1, 4]");
+  FWAV_CHECK_ARG(mode != 4 || (value >= 0.0f && value < 4.0f), FWAV_ERR_ARG,
+                 "fwav_debug_topk_floor: the second pass's margin must lie in [0, 4)");
   FWAV_CHECK_ARG((mode != 1 && mode != 3) || (value == value && value > -INFINITY && value < INFINITY), FWAV_ERR_ARG,
                  "fwav_debug_topk_floor: the forced floor must be finite");
-  g_floor_mode = mode;
+  g_floor_mode = mode == 4 ? 2 : mode;
+  g_floor2_margin = mode == 4 ? value : kFloor2Margin;
   g_floor_rank = mode == 2 && value >= 1.0f && value <= (float)kFloorPilots ? (int)value : kFloorRank;
   uint32_t u;
   std::memcpy(&u, &value, sizeof u);
@@ -3012,8 +3025,8 @@ int fwav_debug_sim_topk_layout(int64_t max_q, int64_t nd, int64_t* offsets) {
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.
 int fwav_debug_topk_plan(int rt, int pieces) {
-  FWAV_CHECK_ARG(pieces == -1 || (pieces >= 1 && pieces <= kPlanMaxPieces), FWAV_ERR_ARG,
-                 "fwav_debug_topk_plan: pieces outside [1, 8] (or -1: query halves)");
+  FWAV_CHECK_ARG(pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces), FWAV_ERR_ARG,
+                 "fwav_debug_topk_plan: pieces outside [1, %d] (or -1: query halves)", kMaxPieces);
   g_plan_rt = rt;
   g_plan_p = rt < 0 ? -1 : pieces;
   return FWAV_OK;

@@ -108,7 +108,7 @@ int fwav_prune(const float* ranges, int64_t n, int64_t q_offset, int range_size,
  * outside the K with the K-th's score (−1: not collected, at most 7), [2 ..] = those domains — the rows whose order
  * (or set) the reference leaves to numpy's argpartition/argsort; see fwav_tie_check.
  * K ≤ 64: emb16 != NULL selects the fp16 MFMA pre-filter + exact f32 rescoring
- * kernel, emb16 == NULL the all-f32 MFMA kernel; both return identical candidates.  (For at least 65,536 queries
+ * kernel, emb16 == NULL the all-f32 MFMA kernel; both return identical candidates.  (For at least 32,768 queries
  * over 65,536 to 4 Mi domains the fp16 search starts every band limit at a floor guessed from pilot queries and
  * searches again, without it, the queries the floor may have cut — all on `stream`, no host synchronisation, the
  * same candidates.)  K > 64 (the module-global

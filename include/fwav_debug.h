@@ -13,7 +13,8 @@ extern "C" {
 
 /* Diagnostic ablations of the fp16 kernel (timing only, outputs invalid for dbg & 65535 != 0); stats (u64[16]
  * device, may be NULL) receives slow-path counters — of the first pass, or with dbg = 1 << 17 of the exact-mode
- * relaunch for overflowed queries only (outputs valid).  Not used by the product path. */
+ * relaunch for overflowed queries only (outputs valid); dbg bit 18 counts in the product's first-pass geometry
+ * (else the base one), bit 19 with the product's speculative floor (else none).  Not used by the product path. */
 int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, const int32_t* active,
                         const int32_t* n_active, int64_t max_q, int64_t q_offset, int k, int32_t* cand,
                         void* workspace, size_t ws_bytes, int dbg, unsigned long long* stats, void* stream);
@@ -50,10 +51,11 @@ int fwav_debug_topk_geometry(int wide);
 int64_t fwav_debug_topk_qb(int geo);
 /* Diagnostic override of the fp16 search's speculative floor (a first pass's band limits start at a floor guessed from
  * pilot queries; the queries it cuts are searched again without it): −1 = the default (first passes of at least
- * 65,536 queries over 65,536 to 4 Mi domains), 0 = never, 1 = every first pass, at the floor `value` (a filter score;
+ * 32,768 queries over 65,536 to 4 Mi domains), 0 = never, 1 = every first pass, at the floor `value` (a filter score;
  * above a query's K-th score it sends the query to the second pass), 2 = every first pass, floor from the pilots
  * (`value` ≥ 1: the pilots' value-th smallest estimate instead of the default rank), 3 = as 1, and the second pass
- * at the same floor (every query the first pass cuts is cut again: the floor-free third pass takes them).
+ * at the same floor (every query the first pass cuts is cut again: the floor-free third pass takes them), 4 = as 2 at
+ * the default rank, with the second pass's floor `value` (≥ 0) below the pilots' smallest estimate instead of 0.15.
  * All return the same candidates. */
 int fwav_debug_topk_floor(int mode, float value);
 /* Diagnostic override of the floor's second pass: table pieces per split block of misses (1 … 32; 0 = the default:

@@ -91,7 +91,7 @@ int main() {
   CHECK(fwav_debug_topk_plan_cover(10, 0, 9, 0, nullptr, nullptr) == FWAV_ERR_ARG, "cover pieces");
   CHECK(fwav_debug_topk_geometry(4) == FWAV_ERR_ARG, "geometry range");
   CHECK(fwav_debug_topk_mode(2) == FWAV_ERR_ARG, "mode range");
-  CHECK(fwav_debug_topk_plan(0, 9) == FWAV_ERR_ARG, "plan pieces");
+  CHECK(fwav_debug_topk_plan(0, 65) == FWAV_ERR_ARG, "plan pieces");
   CHECK(fwav_sim_topk(nullptr, nullptr, 10, nullptr, nullptr, 10, 0, 64, 1, nullptr, nullptr, nullptr, 0, nullptr) ==
             FWAV_ERR_ARG, "sim_topk null");
   void* p = reinterpret_cast<void*>(16);

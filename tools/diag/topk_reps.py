@@ -3,7 +3,7 @@
 apply (FWAV_DEBUG_TOPK_FLOOR="mode[:value]", FWAV_DEBUG_TOPK_GEOMETRY, FWAV_DEBUG_TOPK_P2): a target for
 `rocprofv3 --kernel-trace --stats` per knob setting.  Prints the median call time (HIP events) and the floor's
 miss counts of the last call.
-usage: [AB_NQ=41344] python tools/diag/topk_reps.py [reps]"""
+usage: [AB_NQ=41344] [AB_LO=first query] python tools/diag/topk_reps.py [reps]"""
 from __future__ import annotations
 
 import os
@@ -31,8 +31,9 @@ def main():
     emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
     assert d.fwav_emb16_from_emb(r.emb.data_ptr(), nd, emb16.data_ptr(), st) == 0
     nq = int(os.environ.get("AB_NQ", nr))
-    lo = nr - nq  # the last rank's block (bench.py's roofline_rank_share)
-    active = torch.arange(nq, dtype=torch.int32, device="cuda")
+    # the last rank's block (bench.py's roofline_rank_share), or the block at AB_LO
+    lo = int(os.environ["AB_LO"]) if os.environ.get("AB_LO") else nr - nq
+    active = torch.arange(nq, dtype=torch.int32, device="cuda")  # (cfg2 noise: every range active)
     n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
     wsn = d.fwav_sim_topk_workspace_size(nq, nd, 64)
     wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")

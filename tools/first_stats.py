@@ -1,6 +1,6 @@
 """Counters of the fp16 search's first pass (STATS build of the kernel: replayed chunks, firing tiles, appends,
 compactions, time shares) on cfg2 for the first AB_NQ queries (tools only).
-usage: AB_NQ=41344 python tools/first_stats.py   (AB_DBG=262144: the product's centroid geometry instead of the base)"""
+usage: AB_NQ=41344 python tools/first_stats.py   (AB_DBG=262144: the product's geometry instead of the base; 786432: and its floor)"""
 import os as _os_dbg
 _os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
