@@ -2373,9 +2373,19 @@ constexpr int64_t kFloorMaxD = int64_t(1) << 22;
 // 82,688 queries 4.86 → 4.60 ms with the round's faster pilots and merge, profiles/r06/ab_floor_p2_quarter.log), else
 // 16 (cfg2's ≈ 5,000 misses in 21 blocks × 16 pieces fill one round; 32 pieces would take two)
 constexpr int kFloorP2 = 16, kFloorP2Few = 32;
-constexpr int kFloorPilots = 512;  // pilot queries (evenly spaced over the active list)
-constexpr int kFloorJ = 8;         // the pilot's estimate: its j-th best score over every (K/j)-th domain ≈ its K-th
-constexpr int kFloorRank = 10;    // the floor: the pilots' kFloorRank-th smallest estimate (≈ their 2 % quantile)
+// Pilot count and floor rank (A/B builds may override): 256 pilots at rank 5 (the same ≈ 2 % quantile) against
+// round 5's 512 at rank 10, same process, identical candidates (profiles/r06/ab_pilots256/): cfg2 14.03 → 14.01
+// ms, 165,375 queries 7.83 → 7.87, 82,688 4.55 → 4.48, 41,344 2.85 → 2.80 — the pilots' half of the work (≈ 55 µs)
+#ifndef FWAV_FLOOR_PILOTS
+#define FWAV_FLOOR_PILOTS 256
+#endif
+#ifndef FWAV_FLOOR_RANK
+#define FWAV_FLOOR_RANK 5
+#endif
+constexpr int kFloorPilots = FWAV_FLOOR_PILOTS;  // pilot queries (evenly spaced over the active list)
+constexpr int kFloorJ = 8;  // the pilot's estimate: its j-th best score over every (K/j)-th domain ≈ its K-th
+constexpr int kFloorRank = FWAV_FLOOR_RANK;  // the floor: the pilots' kFloorRank-th smallest estimate (≈ 2 % quantile)
+static_assert(kFloorPilots % 64 == 0 && kFloorPilots <= 1024, "pilots: whole waves, one k_floor_reduce workgroup");
 // second pass: up to kFloorSplit blocks (of 256 misses) split into kFloorP2 pieces, any further ones
 // whole-table (a floor that cut more than 5 % of cfg2's queries)
 constexpr int kFloorSplit = 64;
@@ -2563,6 +2573,8 @@ __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __re
   // every pilot's place in (estimate, pilot) order: the one at place rank − 1 is the floor, the one at place 0 the
   // second pass's floor (+ kFloor2Margin)
   int place = 0;
+  // (unrolled: the LDS reads are independent — the rolled loop waited on each one, 15 µs for 512 pilots)
+#pragma unroll 32
   for (int i = 0; i < kFloorPilots; ++i) {
     const float x = est[i];
     place += (x < e || (x == e && i < p)) ? 1 : 0;

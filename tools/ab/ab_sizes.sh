@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 B=${AB_BASE:-tools/ab/libfwav_prev.so}
-N=audio-compression_amd/fwav/libfwav_debug.so
+N=${AB_NEW:-audio-compression_amd/fwav/libfwav_debug.so}
 tools/gpu_steps.sh \
  "ab_n1:300:python -u tools/lib_ab.py $B $N 9" \
  "ab_n2:300:AB_NQ=165375 python -u tools/lib_ab.py $B $N 11" \

@@ -3,7 +3,7 @@
 apply (FWAV_DEBUG_TOPK_FLOOR="mode[:value]", FWAV_DEBUG_TOPK_GEOMETRY, FWAV_DEBUG_TOPK_P2): a target for
 `rocprofv3 --kernel-trace --stats` per knob setting.  Prints the median call time (HIP events) and the floor's
 miss counts of the last call.
-usage: [AB_NQ=41344] [AB_LO=first query] python tools/diag/topk_reps.py [reps]"""
+usage: [AB_NQ=41344] [AB_LO=first query] [AB_TIES=1] python tools/diag/topk_reps.py [reps]"""
 from __future__ import annotations
 
 import os
@@ -20,7 +20,8 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 9
     import __graft_entry__
     __graft_entry__.build()
-    from fwav import engine, synth, ties
+    from fwav import engine, synth
+    from fwav.nporder import blas_threads
     from fwav._lib import debug_lib, sim_topk_layout
     d = debug_lib()
     sig = torch.from_numpy(synth.noise(60.0, 44100)).cuda()
@@ -38,12 +39,16 @@ def main():
     wsn = d.fwav_sim_topk_workspace_size(nq, nd, 64)
     wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
     cand = torch.empty(nq * 64, dtype=torch.int32, device="cuda")
+    # AB_TIES=1: the search also lists its tied queries (the product's tie_order="numpy" calls pass this list)
+    ties = (torch.empty(d.fwav_tie_list_size(nq), dtype=torch.int32, device="cuda")
+            if os.environ.get("AB_TIES") == "1" else None)
     ms = []
     for i in range(reps + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rc = d.fwav_sim_topk(r.emb.data_ptr(), emb16.data_ptr(), nd, active.data_ptr(), n_active.data_ptr(), nq, lo,
-                             64, ties.blas_threads(), cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
+                             64, blas_threads(), cand.data_ptr(), None if ties is None else ties.data_ptr(), wsk.data_ptr(),
+                             wsn, st)
         e1.record()
         torch.cuda.synchronize()
         assert rc == 0
@@ -55,7 +60,8 @@ def main():
     same = bool(torch.equal(cand, ref)) if r.n_resolved == 0 else None
     print(f"{nq} queries: median {np.median(ms):.3f} ms (min {min(ms):.3f}); floor misses {cnt('n_miss')} / "
           f"{cnt('n_miss2')}; env floor={os.environ.get('FWAV_DEBUG_TOPK_FLOOR', '-')} "
-          f"geometry={os.environ.get('FWAV_DEBUG_TOPK_GEOMETRY', '-')}; equal to the product rows: {same}", flush=True)
+          f"geometry={os.environ.get('FWAV_DEBUG_TOPK_GEOMETRY', '-')}; equal to the product rows: {same}"
+          + (f"; tied queries {int(ties[0].item())}" if ties is not None else ""), flush=True)
 
 
 if __name__ == "__main__":
