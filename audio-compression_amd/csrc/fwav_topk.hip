@@ -43,13 +43,14 @@
 #if !defined(FWAV_DEBUG_API) && (defined(FWAV_TOPK_ABL) || defined(FWAV_TOPK_APPOFF) || defined(FWAV_TOPK_CAP) || \
     defined(FWAV_TOPK_CB) || defined(FWAV_TOPK_CENT) || defined(FWAV_TOPK_CENTWIDE) || defined(FWAV_TOPK_CENT_HL) || \
     defined(FWAV_TOPK_CENT_MINQ) || defined(FWAV_TOPK_CG) || defined(FWAV_TOPK_CHAINS) || \
-    defined(FWAV_TOPK_CPDBL) || defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || defined(FWAV_TOPK_CVACC) || \
+    defined(FWAV_TOPK_CPDBL) || defined(FWAV_TOPK_CPMIN) || defined(FWAV_TOPK_CSHARE) || defined(FWAV_TOPK_BANDB) || defined(FWAV_TOPK_CVACC) || \
     defined(FWAV_TOPK_CW) || defined(FWAV_TOPK_CWPE) || defined(FWAV_TOPK_DELTA) || defined(FWAV_TOPK_EXGROW) || \
     defined(FWAV_TOPK_EXWPE) || defined(FWAV_TOPK_FIRST) || defined(FWAV_TOPK_G) || defined(FWAV_TOPK_GROW) || \
     defined(FWAV_TOPK_HLDELTA) || defined(FWAV_TOPK_HLPRE) || defined(FWAV_TOPK_INTERLEAVE) || \
     defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
     defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || \
-    defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE))
+    defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE) || \
+    defined(FWAV_FLOOR_PILOTS) || defined(FWAV_FLOOR_RANK))
 #error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
 #endif
 
@@ -839,20 +840,35 @@ __device__ __forceinline__ void compact16(uint64_t* __restrict__ kq, SM& sm, int
 // every exact top-K member's key is above it), written densely at the front of its buffer, and a header in the last
 // slot: (overflow key << 32) | count.  k_merge_pieces rescores and sorts the union of the pieces' bands once per
 // query.  A band that would not leave 64 slots is flagged as overflowed (the query goes to the exact-mode relaunch).
-template <int C, bool HL, class SM>
-__device__ __forceinline__ void piece_band(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
-                                           uint32_t* __restrict__ share_q) {
+// The band's keys of query ql (n = its entries, 0 past them), loaded by piece_band_load — for kBandBatch queries at
+// once, so that the final loop of a table piece pays one memory round trip per batch instead of two per query
+// (round 6, same process, identical candidates, profiles/r06/ab_band_batch.log: 330,750 / 165,375 / 82,688 / 41,344
+// queries 14.49 → 14.38 / 8.07 → 7.86 / 4.48 → 4.37 / 2.82 → 2.72 ms)
+#ifndef FWAV_TOPK_BANDB
+#define FWAV_TOPK_BANDB 4
+#endif
+constexpr int kBandBatch = FWAV_TOPK_BANDB;
+template <int C, class SM>
+__device__ __forceinline__ int piece_band_load(const uint64_t* __restrict__ kq, SM& sm, int ql,
+                                               uint64_t (&v)[C / 64]) {
   constexpr int E = C / 64;
   const int lane = threadIdx.x & 63;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int n0 = sm.cnt[ql];
   const int n = min(n0 + sm.cnt1[ql], C);
-  uint64_t v[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const int e = j * 64 + lane;
     v[j] = e < n ? ld_key(kq + two_end_slot<C>(e, n0)) : 0ull;
   }
+  return n;
+}
+// sh0: the query's shared limit read with its keys (any earlier value is a valid, smaller lower bound)
+template <int C, bool HL, class SM>
+__device__ __forceinline__ void piece_band(uint64_t* __restrict__ kq, SM& sm, int ql, int K,
+                                           uint32_t* __restrict__ share_q, uint64_t (&v)[C / 64], int n,
+                                           uint32_t sh0) {
+  constexpr int E = C / 64;
+  const int lane = threadIdx.x & 63;
   // the piece's own limit now (a last compaction's select over its whole buffer), published before the filter so
   // that the pieces still streaming and k_merge_pieces see it
   uint32_t Lk = 0u;
@@ -868,7 +884,7 @@ __device__ __forceinline__ void piece_band(uint64_t* __restrict__ kq, SM& sm, in
     Lk = f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta);
     if (lane == 0) atomicMax(share_q, Lk);
   }
-  Lk = max(Lk, __hip_atomic_load(share_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  Lk = max(Lk, sh0);
   int m = 0;
 #pragma unroll
   for (int j = 0; j < E; ++j) {
@@ -1664,12 +1680,21 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     nfired[s] = qcnt[s] = kept[s] = 0;
     cur[s] = ReplayCursor{0, 0, 0u};
   }
+  // CENT: the pieces' shared limits, loaded before each group's top wait and applied before the next group's DMA is
+  // issued.  (Read after that issue, as rounds 4–5 did, the compiler's wait for the loaded value, vmcnt(0), also
+  // waited for the whole next group's DMA: every group's level 1 started only once the group after it had landed.)
+  uint32_t shv[QS];
   for (int g = 0; g < ngroups; ++g) {
     u32x4(*half)[512] = slots + (g % NB) * G;
     const int cg = c0 + g * G;  // first chunk of group g
     const int c_end = cg + G < c1 ? cg + G : c1;
     const bool window_end =
         (c_end - c0 <= kWarmChunks) || ((g + 1) % (kWindowGroups * 4 / G) == 0) || (g + 1 == ngroups);
+    if (CENT && FWAV_TOPK_CSHARE && share != nullptr) {
+#pragma unroll
+      for (int s = 0; s < QS; ++s)
+        shv[s] = __hip_atomic_load(share + qpos[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const unsigned long long t_b0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     // RAW: own DMA of group g retired, then every wave's (barrier).  WAR: the other half was last read in
     // iteration g−1, whose ds_reads were all consumed before its waves reached this barrier.
@@ -1682,17 +1707,16 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     }
     const unsigned long long t_b1 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(7, t_b1 - t_b0);
+    if (CENT && FWAV_TOPK_CSHARE && share != nullptr) {
+      // CENT: the pieces' shared limits every group (a filter threshold that rises sooner skips more level-2 work),
+      // retired by the wait above
+#pragma unroll
+      for (int s = 0; s < QS; ++s)
+        if (upd[s] && shv[s] != 0u) thf[s] = fmaxf(thf[s], key2f(shv[s]));
+    }
     // (the DMA issued after level 1 or level 2 instead measured no better: profiles/r04/ab_prefix_dma_barrier.log)
     if (g + 1 < ngroups) issue_group(g + 1);
     if (ABL && (dbg & 2)) continue;
-    if (CENT && FWAV_TOPK_CSHARE && share != nullptr) {
-      // CENT: the pieces' shared limits every group (a filter threshold that rises sooner skips more level-2 work)
-#pragma unroll
-      for (int s = 0; s < QS; ++s) {
-        const uint32_t v = __hip_atomic_load(share + qpos[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (upd[s] && v != 0u) thf[s] = fmaxf(thf[s], key2f(v));
-      }
-    }
     int thi[QS];
 #pragma unroll
     for (int s = 0; s < QS; ++s) thi[s] = int_threshold(HL ? thf[s] - kStreamMargin : thf[s]);
@@ -1809,7 +1833,8 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
     const unsigned long long t_c = STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     if (STATS) stat_add(9, t_c - t_b1);
     if (window_end) {
-      if (share != nullptr) {  // the largest limit the query's pieces have published
+      // the largest limit the query's pieces have published (CENT reads it every group, above)
+      if (share != nullptr && !(CENT && FWAV_TOPK_CSHARE)) {
 #pragma unroll
         for (int s = 0; s < QS; ++s) {
           const uint32_t v = __hip_atomic_load(share + qpos[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1846,20 +1871,45 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
       sm.cnt1[lid[s] * 32 + col] = qcnt[s];
   }
 
-  for (int l = 0; l < 32 * QS; ++l) {
+  auto slot_of = [&](int l) {  // the wave's l-th query slot
     int ls = lid[0];
 #pragma unroll
     for (int s = 1; s < QS; ++s) ls = (l >> 5) == s ? lid[s] : ls;
-    const int qs = ls * 32 + (l & 31);
+    return ls * 32 + (l & 31);
+  };
+  if (npieces > 1) {
+    // a table piece hands each query's filtered band to k_merge_pieces: kBandBatch queries' keys and shared limits
+    // loaded together (the wave's own appends drained once)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int l0 = 0; l0 < 32 * QS; l0 += kBandBatch) {
+      uint64_t v[kBandBatch][C / 64];
+      int nb_[kBandBatch];
+      uint32_t sh[kBandBatch];
+#pragma unroll
+      for (int b = 0; b < kBandBatch; ++b) {
+        const int qs = slot_of(l0 + b);
+        const int64_t qq = slot_query(block, qslot0 + qs, plan.nb, QB);
+        const bool ok = l0 + b < 32 * QS && qq < n_active;
+        nb_[b] = ok ? piece_band_load<C>(gkeys + (size_t)qs * C, sm, qs, v[b]) : -1;
+        sh[b] = ok ? __hip_atomic_load(share_lim + qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      }
+#pragma unroll
+      for (int b = 0; b < kBandBatch; ++b) {
+        if (nb_[b] < 0) continue;
+        const int qs = slot_of(l0 + b);
+        const int64_t qq = slot_query(block, qslot0 + qs, plan.nb, QB);
+        if (lane == 0) FWAV_TRACE(sm.qrow[qs], 3u, (uint32_t)sm.cnt[qs], (uint32_t)sm.ovf[qs], (uint32_t)sm.cnt1[qs]);
+        piece_band<C, HL>(gkeys + (size_t)qs * C, sm, qs, K, share_lim + qq, v[b], nb_[b], sh[b]);
+      }
+    }
+  }
+  for (int l = 0; l < (npieces > 1 ? 0 : 32 * QS); ++l) {
+    const int qs = slot_of(l);
     const int64_t qq = slot_query(block, qslot0 + qs, plan.nb, QB);
     if (qq >= n_active) continue;
     const int32_t qid = active[qq];
     uint64_t* kq = gkeys + (size_t)qs * C;
     if (lane == 0) FWAV_TRACE(sm.qrow[qs], 3u, (uint32_t)sm.cnt[qs], (uint32_t)sm.ovf[qs], (uint32_t)sm.cnt1[qs]);
-    if (npieces > 1) {  // a table piece hands its filtered band to k_merge_pieces
-      piece_band<C, HL>(kq, sm, qs, K, share_lim + qq);
-      continue;
-    }
     // exact f32 rescoring of the kept band + sort
     compact16<C>(kq, sm, qs, K, emb, cand + (int64_t)qid * K, sp, ties, qid, fkey, fl);
     // overflowed: listed for the exact-mode relaunch with its band limit as the seed (same list position)
