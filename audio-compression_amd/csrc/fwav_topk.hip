@@ -2446,6 +2446,9 @@ constexpr int kFloorSplit = 64;
 // pieces do not start cold either; the queries that one cuts (normally none) take a floor-free third pass.  (Full
 // score rows for them, launch_topk_large, measured 3.6 ms per launch: one workgroup per row streams it repeatedly.)
 constexpr float kFloor2Margin = 0.15f;
+// (The later passes in the centroid geometry, on the miss list in its atomic order, measured slower: 330,750 /
+// 165,375 / 82,688 / 41,344 queries 14.14 → 14.70 / 7.72 → 8.13 / 4.38 → 4.78 / 2.69 → 3.20 ms, round 6,
+// profiles/r06/ab_floor_geo2.log — consecutive misses are unrelated queries, so the centroids' slack is large.)
 static_assert(kFloorP2 >= 1 && kFloorP2Few <= kMaxPieces, "second-pass pieces outside the merge");
 #ifdef FWAV_DEBUG_API
 static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 / 3 forced value, 2 pilot at any size
