@@ -2023,10 +2023,11 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
 // and, up to merge_fast(MP)·64 of them, selected from registers; a wider union (long runs of near-equal scores) is
 // selected by re-reading it from L2 once per key bit instead, so the register budget — and the occupancy — no longer
 // scale with the widest plan's P·(C − 64).
-// (The floor's second pass merges 16 or 32 pieces of a low floor: its unions above Lk run to ≈ 800 entries and more;
-// there the union's key words, merge_hi_rows(MP) rows of them, are selected from LDS before the L2 tier.)
+// (The floor's second pass merges 16, 32 or 64 pieces of a low floor: its unions above Lk run to ≈ 800 entries and
+// more — thousands with 64 pieces; there the union's key words, merge_hi_rows(MP) rows of them, are selected from LDS
+// before the L2 tier: a 64-piece merge of 580 queries 786 µs with 32 rows, 145 with 64.)
 constexpr int kMergeFast = 8;
-constexpr int merge_hi_rows(int MP) { return MP <= 8 ? 1 : 32; }
+constexpr int merge_hi_rows(int MP) { return MP <= 8 ? 1 : (MP <= 32 ? 32 : 64); }
 template <int C, int QB, bool HL, int MP>
 __global__ __launch_bounds__(256) void k_merge_pieces(const uint64_t* __restrict__ gkeys_all,
                                                       const int32_t* __restrict__ active,
@@ -2171,9 +2172,18 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
 #pragma unroll 1
         for (int bit = top; bit >= kBit0; --bit) {
           const uint32_t Tc = T | (1u << bit);
+          // the lane's count over the rows, 8 LDS reads in flight, then one wave sum per bit
           int c = 0;
 #pragma unroll 1
-          for (int u = 0; u < mu; ++u) c += __popcll(__ballot(u * 64 + lane < m && sh[u * 64 + lane] >= Tc));
+          for (int u0 = 0; u0 < mu; u0 += 8) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const int e = (u0 + i) * 64 + lane;
+              c += (e < m && sh[e < kHiRows * 64 ? e : 0] >= Tc) ? 1 : 0;
+            }
+          }
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
           if (c >= K) T = Tc;
         }
         L = max(L, f2key(HL ? key2f(T) - 2.5f * kHLDelta : key2f(T) - 2.0f * kF16Delta));
@@ -2418,11 +2428,12 @@ constexpr int64_t kFloorMinQ = 32768, kFloorMinD = 65536;
 // 86.4 M domains the second pass took 204 ms after a 511 ms first pass (a 262,144-query search, profiles/r05/
 // kernel_stats_bench_cfg2.txt: the cfg4 affine-roofline extra of bench.py)
 constexpr int64_t kFloorMaxD = int64_t(1) << 22;
-// the second pass's table pieces per split block: 32 where the misses expected at the floor's rank (≈ 2 % of the
-// launch) fill at most one round of workgroup slots in 32 pieces (the pass's latency is the length of one piece:
-// 82,688 queries 4.86 → 4.60 ms with the round's faster pilots and merge, profiles/r06/ab_floor_p2_quarter.log), else
-// 16 (cfg2's ≈ 5,000 misses in 21 blocks × 16 pieces fill one round; 32 pieces would take two)
-constexpr int kFloorP2 = 16, kFloorP2Few = 32;
+// the second pass's table pieces per split block: the most of 64 / 32 / 16 with which the misses expected at the
+// floor's rank (≈ 2 % of the launch) fill at most one round of workgroup slots (the pass's latency is the length of
+// one piece: 82,688 queries 4.86 → 4.60 ms with 32 instead of 16, profiles/r06/ab_floor_p2_quarter.log; 41,344: 64
+// pieces 370 → 231 µs, their merge 67 → 145 µs, profiles/r06/timeline_eg_41344_f-_g-_p{32,64}.txt); cfg2's ≈ 5,000
+// misses in 21 blocks × 16 pieces fill one round, 32 pieces would take two
+constexpr int kFloorP2 = 16, kFloorP2Few = 32, kFloorP2Fewest = 64;
 // Pilot count and floor rank (A/B builds may override): 256 pilots at rank 5 (the same ≈ 2 % quantile) against
 // round 5's 512 at rank 10, same process, identical candidates (profiles/r06/ab_pilots256/): cfg2 14.03 → 14.01
 // ms, 165,375 queries 7.83 → 7.87, 82,688 4.55 → 4.48, 41,344 2.85 → 2.80 — the pilots' half of the work (≈ 55 µs)
@@ -2449,7 +2460,7 @@ constexpr float kFloor2Margin = 0.15f;
 // (The later passes in the centroid geometry, on the miss list in its atomic order, measured slower: 330,750 /
 // 165,375 / 82,688 / 41,344 queries 14.14 → 14.70 / 7.72 → 8.13 / 4.38 → 4.78 / 2.69 → 3.20 ms, round 6,
 // profiles/r06/ab_floor_geo2.log — consecutive misses are unrelated queries, so the centroids' slack is large.)
-static_assert(kFloorP2 >= 1 && kFloorP2Few <= kMaxPieces, "second-pass pieces outside the merge");
+static_assert(kFloorP2 >= 1 && kFloorP2Fewest <= kMaxPieces, "second-pass pieces outside the merge");
 #ifdef FWAV_DEBUG_API
 static int g_floor_mode = -1;      // fwav_debug_topk_floor: −1 auto, 0 off, 1 / 3 forced value, 2 pilot at any size
 static uint32_t g_floor_key = 0u;
@@ -2479,7 +2490,10 @@ static void floor_plan(int64_t max_q, int64_t nd, int& rt, int& P) {
   int cus, per_cu;
   topk_device_slots(kGeoBase, cus, per_cu);
   const int64_t blocks = cdiv(cdiv(max_q > 0 ? max_q : 1, 50), k16QB);  // ≈ 2 % of the launch, in 256-query blocks
-  const int p2 = g_floor_p2 > 0 ? g_floor_p2 : (blocks * kFloorP2Few <= (int64_t)cus * per_cu ? kFloorP2Few : kFloorP2);
+  const int64_t slots = (int64_t)cus * per_cu;
+  const int p2 = g_floor_p2 > 0 ? g_floor_p2
+                                : (blocks * kFloorP2Fewest <= slots ? kFloorP2Fewest
+                                                                    : (blocks * kFloorP2Few <= slots ? kFloorP2Few : kFloorP2));
   P = (int)std::max<int64_t>(1, std::min<int64_t>(p2, pmax));
 }
 

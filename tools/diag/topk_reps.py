@@ -3,7 +3,7 @@
 apply (FWAV_DEBUG_TOPK_FLOOR="mode[:value]", FWAV_DEBUG_TOPK_GEOMETRY, FWAV_DEBUG_TOPK_P2): a target for
 `rocprofv3 --kernel-trace --stats` per knob setting.  Prints the median call time (HIP events) and the floor's
 miss counts of the last call.
-usage: [AB_NQ=41344] [AB_LO=first query] [AB_TIES=1] python tools/diag/topk_reps.py [reps]"""
+usage: [AB_NQ=41344] [AB_LO=first query] [AB_TIES=1] [AB_PLAN=rt,P] python tools/diag/topk_reps.py [reps]"""
 from __future__ import annotations
 
 import os
@@ -31,6 +31,8 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device="cuda")
     assert d.fwav_emb16_from_emb(r.emb.data_ptr(), nd, emb16.data_ptr(), st) == 0
+    if os.environ.get("AB_PLAN"):  # "rt,pieces": the work-plan override (fwav_debug_topk_plan), before sizing
+        assert d.fwav_debug_topk_plan(*[int(x) for x in os.environ["AB_PLAN"].split(",")]) == 0
     nq = int(os.environ.get("AB_NQ", nr))
     # the last rank's block (bench.py's roofline_rank_share), or the block at AB_LO
     lo = int(os.environ["AB_LO"]) if os.environ.get("AB_LO") else nr - nq
@@ -60,7 +62,7 @@ def main():
     same = bool(torch.equal(cand, ref)) if r.n_resolved == 0 else None
     print(f"{nq} queries: median {np.median(ms):.3f} ms (min {min(ms):.3f}); floor misses {cnt('n_miss')} / "
           f"{cnt('n_miss2')}; env floor={os.environ.get('FWAV_DEBUG_TOPK_FLOOR', '-')} "
-          f"geometry={os.environ.get('FWAV_DEBUG_TOPK_GEOMETRY', '-')}; equal to the product rows: {same}"
+          f"geometry={os.environ.get('FWAV_DEBUG_TOPK_GEOMETRY', '-')} plan={os.environ.get('AB_PLAN', '-')}; equal to the product rows: {same}"
           + (f"; tied queries {int(ties[0].item())}" if ties is not None else ""), flush=True)
 
 
