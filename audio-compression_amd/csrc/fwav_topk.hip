@@ -2080,28 +2080,60 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
   const uint64_t hdr = lane < P ? gkeys_all[base0 + (int64_t)lane * pstride + C - 1] : 0ull;
   const uint32_t Lk = __builtin_amdgcn_readfirstlane(share[qq]);
   const int32_t qid = __builtin_amdgcn_readfirstlane(active[qq]);
-  // prefix of the counts (wave-uniform) and the largest overflow flag
-  int pre[MP + 1];
+  // prefix of the counts and the largest overflow flag.  Up to 16 pieces: wave-uniform, in SGPRs, and a piece found by
+  // comparing against each prefix; 32 / 64 pieces: lane p holds piece p's exclusive prefix and an entry's piece is
+  // found by a binary search over the lanes (6 shuffles instead of MP − 1 compares and selects per entry)
+  constexpr bool kLanePre = MP > 16;
+  int pre[kLanePre ? 1 : MP + 1];
   uint32_t seed = 0u;
-  pre[0] = 0;
+  int n = 0, pre_l = 0;
+  if constexpr (kLanePre) {
+    static_assert(MP <= 64, "one piece per lane");
+    const int cnt = lane < P ? (int)(uint32_t)hdr : 0;
+    int inc = cnt;  // inclusive prefix over the lanes
 #pragma unroll
-  for (int p = 0; p < MP; ++p) {
-    const uint64_t h = p < P ? (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)hdr, p) |
-                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hdr >> 32), p) << 32)
-                             : 0ull;
-    seed = max(seed, (uint32_t)(h >> 32));
-    pre[p + 1] = pre[p] + (int)(uint32_t)h;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(inc, off);
+      if (lane >= off) inc += y;
+    }
+    pre_l = inc - cnt;
+    n = __builtin_amdgcn_readlane(inc, 63);
+    uint32_t sd = lane < P ? (uint32_t)(hdr >> 32) : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sd = max(sd, (uint32_t)__shfl_xor((int)sd, off));
+    seed = __builtin_amdgcn_readfirstlane(sd);
+  } else {
+    pre[0] = 0;
+#pragma unroll
+    for (int p = 0; p < MP; ++p) {
+      const uint64_t h = p < P ? (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)hdr, p) |
+                                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hdr >> 32), p) << 32)
+                               : 0ull;
+      seed = max(seed, (uint32_t)(h >> 32));
+      pre[p + 1] = pre[p] + (int)(uint32_t)h;
+    }
+    n = pre[MP];
   }
-  const int n = pre[MP];
   // entry e of the union: piece p (pre[p] ≤ e < pre[p + 1]) at offset e − pre[p]; 0 past the end
   auto entry = [&](int e) -> uint64_t {
     int p = 0, start = 0;
+    if constexpr (kLanePre) {
+      // the largest p < P with pre[p] ≤ e (a piece of count 0 shares its prefix with the next one, which wins)
 #pragma unroll
-    for (int pp = 1; pp < MP; ++pp)
-      if (pp < P && e >= pre[pp]) {
-        p = pp;
-        start = pre[pp];
+      for (int step = 32; step > 0; step >>= 1) {
+        const int mid = p + step;
+        const int pm = __shfl(pre_l, mid < 64 ? mid : 63);
+        if (mid < P && pm <= e) p = mid;
       }
+      start = __shfl(pre_l, p);
+    } else {
+#pragma unroll
+      for (int pp = 1; pp < MP; ++pp)
+        if (pp < P && e >= pre[pp]) {
+          p = pp;
+          start = pre[pp];
+        }
+    }
     return e < n ? gkeys_all[base0 + (int64_t)p * pstride + (e - start)] : 0ull;
   };
   const int nu = (n + 63) >> 6;  // 64-entry rows of the union (wave-uniform)
