@@ -3,7 +3,7 @@
 apply (FWAV_DEBUG_TOPK_FLOOR="mode[:value]", FWAV_DEBUG_TOPK_GEOMETRY, FWAV_DEBUG_TOPK_P2): a target for
 `rocprofv3 --kernel-trace --stats` per knob setting.  Prints the median call time (HIP events) and the floor's
 miss counts of the last call.
-usage: [AB_NQ=41344] [AB_LO=first query] [AB_TIES=1] [AB_PLAN=rt,P] python tools/diag/topk_reps.py [reps]"""
+usage: [AB_NQ=41344] [AB_LO=first query] [AB_TIES=1] [AB_PLAN=rt,P] [AB_RUNS=1 | AB_ENGINE_ACTIVE=1] python tools/diag/topk_reps.py [reps]"""
 from __future__ import annotations
 
 import os
@@ -37,6 +37,15 @@ def main():
     # the last rank's block (bench.py's roofline_rank_share), or the block at AB_LO
     lo = int(os.environ["AB_LO"]) if os.environ.get("AB_LO") else nr - nq
     active = torch.arange(nq, dtype=torch.int32, device="cuda")  # (cfg2 noise: every range active)
+    if os.environ.get("AB_RUNS") == "1":  # fwav_prune's order: runs of 64 consecutive ranges in a random run order
+        g = torch.Generator().manual_seed(0)
+        runs = torch.randperm((nq + 63) // 64, generator=g)
+        active = torch.cat([torch.arange(r * 64, min(nq, r * 64 + 64), dtype=torch.int32) for r in runs.tolist()]).cuda()
+    elif os.environ.get("AB_ENGINE_ACTIVE") == "1":  # the product's own active list of this block
+        rb = engine.compress_device(sig, 2048, 64, shard=(nr - nq, nr), keep_intermediates=True)
+        torch.cuda.synchronize()
+        active = rb.active[:int(rb.n_active.item())].clone()
+        assert active.numel() == nq
     n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
     wsn = d.fwav_sim_topk_workspace_size(nq, nd, 64)
     wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
