@@ -2684,6 +2684,93 @@ __global__ __launch_bounds__(kFloorPilots) void k_floor_reduce(const float* __re
   if (place == 0) floor_key[1] = ok ? f2key(e - margin2) : 0u;
 }
 
+// ------------------------------------------------------------------------------------ the active list in order
+// The search works on its own copy of the active list in ascending query order, whatever order the caller's list is
+// in: fwav_prune appends each wave's ranges (ascending) at an atomic offset, so its list is runs of 64 ascending
+// ranges in arbitrary run order, and with it the first pass ran 2.30 instead of 1.90 ms for 41,344 queries at the
+// same floor (round 6, tools/diag/topk_reps.py AB_RUNS=1 against ascending ranges, profiles/r06/active_order.log;
+// the counters of the two runs' work — appends, level-2 pairs — are equal, so it is how the work lands on the
+// workgroups, not how much of it there is: with ascending ids the interleaved query groups of every block are spread
+// evenly over the queries, with runs in random order each block draws its 16 groups at random and the slowest block
+// sets the launch).  A bitmap of the listed ids (duplicates collapse), one count per 8,192 ids, then every block
+// writes its ids at its prefix: three small kernels, no host synchronisation.  A list holding an id outside
+// [0, max_q) (max_q bounds the list's length, not its ids: a slice of a longer list) is used as given.
+constexpr int kOrderWords = 256;  // bitmap words (8,192 query ids) per block of k_order_sum / k_order_emit
+__host__ __device__ inline int64_t order_words(int64_t max_q) { return cdiv(max_q > 0 ? max_q : 1, 32); }
+// n_order[1] (zeroed with the bitmap): set when an id lies outside [0, max_q)
+__global__ __launch_bounds__(256) void k_order_mark(const int32_t* __restrict__ active,
+                                                    const int32_t* __restrict__ n_active_p, int64_t max_q,
+                                                    uint32_t* __restrict__ bits, int32_t* __restrict__ n_order) {
+  const int64_t n = *n_active_p;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int32_t v = active[i];
+    if (v >= 0 && v < max_q) atomicOr(bits + (v >> 5), 1u << (v & 31));
+    else n_order[1] = 1;
+  }
+}
+// an id outside [0, max_q): the caller's list as given
+__global__ __launch_bounds__(256) void k_order_copy(const int32_t* __restrict__ active,
+                                                    const int32_t* __restrict__ n_active_p,
+                                                    int32_t* __restrict__ order, int32_t* __restrict__ n_order) {
+  if (n_order[1] == 0) return;
+  const int64_t n = *n_active_p;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) order[i] = active[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) n_order[0] = (int32_t)n;
+}
+__device__ __forceinline__ int block_sum256(int c, int* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if (lane == 0) red[wave] = c;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+__global__ __launch_bounds__(256) void k_order_sum(const uint32_t* __restrict__ bits, int64_t nwords,
+                                                   uint32_t* __restrict__ bsum) {
+  __shared__ int red[4];
+  const int64_t w = (int64_t)blockIdx.x * kOrderWords + threadIdx.x;
+  const int t = block_sum256(w < nwords ? __popc(bits[w]) : 0, red);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = (uint32_t)t;
+}
+__global__ __launch_bounds__(256) void k_order_emit(const uint32_t* __restrict__ bits, int64_t nwords,
+                                                    const uint32_t* __restrict__ bsum, int32_t* __restrict__ order,
+                                                    int32_t* __restrict__ n_order) {
+  __shared__ int red[4], wsum[4];
+  if (n_order[1] != 0) return;  // k_order_copy writes the list
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int before = 0;  // ids in the blocks before this one
+  for (int b = tid; b < (int)blockIdx.x; b += 256) before += (int)bsum[b];
+  before = block_sum256(before, red);
+  const int64_t w = (int64_t)blockIdx.x * kOrderWords + tid;
+  const uint32_t word = w < nwords ? bits[w] : 0u;
+  const int c = __popc(word);
+  int inc = c;  // inclusive prefix over the wave's lanes
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(inc, off);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  int pos = before + inc - c;
+  for (int k = 0; k < wave; ++k) pos += wsum[k];
+  for (uint32_t m = word; m != 0u; m &= m - 1u) order[pos++] = (int32_t)(w * 32 + __builtin_ctz(m));
+  if (blockIdx.x == gridDim.x - 1 && tid == 255) *n_order = pos;
+}
+// the caller's active list → order[0 .. *n_order), ascending (workspace regions of TopkLayout)
+static void order_active(const int32_t* active, const int32_t* n_active, int64_t max_q, uint32_t* bits, uint32_t* bsum,
+                         int32_t* order, int32_t* n_order, hipStream_t st) {
+  const int64_t nw = order_words(max_q);
+  const int64_t nb = cdiv(nw, kOrderWords);
+  (void)hipMemsetAsync(bits, 0, (size_t)nw * sizeof(uint32_t), st);
+  (void)hipMemsetAsync(n_order + 1, 0, sizeof(int32_t), st);
+  const int64_t gm = std::min<int64_t>(cdiv(max_q > 0 ? max_q : 1, 256), 2048);
+  k_order_mark<<<gm, 256, 0, st>>>(active, n_active, max_q, bits, n_order);
+  k_order_sum<<<nb, 256, 0, st>>>(bits, nw, bsum);
+  k_order_emit<<<nb, 256, 0, st>>>(bits, nw, bsum, order, n_order);
+  k_order_copy<<<gm, 256, 0, st>>>(active, n_active, order, n_order);
+}
+
 // Key-buffer bytes: enough for the first pass in either geometry (a diagnostic override may switch it between the
 // size query and the launch), for the relaunches' base plan and for the floor's second pass.
 static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
@@ -2712,11 +2799,14 @@ static size_t f16_keys_bytes(int64_t max_q, int64_t nd) {
 //   ovf1      i32[q] overflow list of the first pass   n_ovf1  i32 count, then seeds1 u32[q]
 //   miss      i32[q] floor misses of the first pass    n_miss  i32
 //   miss2     i32[q] floor misses of the second pass   n_miss2 i32
-//   floor_key u32[2]                                    pilot   f32 pilot scores + estimates (only when the floor
-//                                                       can run: floor_by_default, or any size in the debug library)
+//   floor_key u32[2]
+//   order     i32[q] the active list in ascending query order (k_order_*), n_order i32[2] its length, a flag
+//   order_bits u32[⌈q/32⌉] its bitmap                  order_bsum u32 per 8,192 queries: the bitmap's block counts
+//   pilot     f32 pilot scores + estimates (only when the floor can run: floor_by_default, or any size in the debug
+//             library)
 struct TopkLayout {
-  size_t keys, share, ovf2, n_ovf2, seeds2, ovf1, n_ovf1, seeds1, miss, n_miss, miss2, n_miss2, floor_key, pilot,
-      total;
+  size_t keys, share, ovf2, n_ovf2, seeds2, ovf1, n_ovf1, seeds1, miss, n_miss, miss2, n_miss2, floor_key, order,
+      n_order, order_bits, order_bsum, pilot, total;
 };
 constexpr size_t kPilotBytes = ((size_t)kFloorPilots * kFloorSlices * kFloorJ + kFloorPilots) * sizeof(float);
 static TopkLayout topk_layout(int64_t max_q, int64_t nd) {
@@ -2735,7 +2825,11 @@ static TopkLayout topk_layout(int64_t max_q, int64_t nd) {
   L.miss2 = L.n_miss + 4;
   L.n_miss2 = L.miss2 + 4 * q;
   L.floor_key = L.n_miss2 + 4;
-  L.pilot = L.floor_key + 8;
+  L.order = L.floor_key + 8;
+  L.n_order = L.order + 4 * q;
+  L.order_bits = L.n_order + 8;
+  L.order_bsum = L.order_bits + 4 * (size_t)order_words(q);
+  L.pilot = L.order_bsum + 4 * (size_t)cdiv((int64_t)order_words(q), kOrderWords);
 #ifdef FWAV_DEBUG_API
   const bool pilots = true;  // a debug knob may force the floor after the size query
 #else
@@ -2880,6 +2974,11 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     // Speculative floor (FloorCtl): from the exact scores of kFloorPilots evenly spaced queries against every
     // (K/8)-th domain (k_floor_pilot), a guess at the lowest K-th score of the search; the queries it may cut are
     // searched again at a lower floor, and the few that one cuts without any (base geometry, table pieces).
+    // the search's own ascending copy of the caller's active list (order_active): every pass below reads it
+    int32_t* const order = reinterpret_cast<int32_t*>(wb + lay.order);
+    int32_t* const n_order = reinterpret_cast<int32_t*>(wb + lay.n_order);
+    order_active(active, n_active, max_q, reinterpret_cast<uint32_t*>(wb + lay.order_bits),
+                 reinterpret_cast<uint32_t*>(wb + lay.order_bsum), order, n_order, st);
     const int fmode = floor_mode();
     // (counter launches run without the floor unless dbg bit 19 asks for the product's floor too)
     const bool use_floor = (!stats_first || (dbg & (1 << 19))) && K <= 64 && floor_by_default(max_q, nd);
@@ -2895,16 +2994,16 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
       } else {
         const int j = K < kFloorJ ? K : kFloorJ, stride = K / j;
         float* est = pilot + (size_t)kFloorPilots * kFloorSlices * kFloorJ;
-        k_floor_pilot<<<kPilotGroups * kFloorSlices, 256, 0, st>>>(emb, nd, active, n_active, q_offset, stride, pilot);
+        k_floor_pilot<<<kPilotGroups * kFloorSlices, 256, 0, st>>>(emb, nd, order, n_order, q_offset, stride, pilot);
         k_floor_est<<<kFloorPilots, 64, 0, st>>>(pilot, kFloorSlices, j, est);
-        k_floor_reduce<<<1, kFloorPilots, 0, st>>>(est, g_floor_rank, n_active, fmode == 2 ? 0 : (int)kFloorMinQ,
+        k_floor_reduce<<<1, kFloorPilots, 0, st>>>(est, g_floor_rank, n_order, fmode == 2 ? 0 : (int)kFloorMinQ,
                                                    g_floor2_margin, floor_key);
       }
       int rt_nf, P_nf;  // the plan when the device finds the floor does not apply
       host_plan_for(max_q, nd, geo, rt_nf, P_nf, 0);
       fl = FloorCtl{floor_key, miss, n_miss, rt_nf, P_nf};
     }
-    first_pass(active, n_active, geo, rt, P, fl, true);
+    first_pass(order, n_order, geo, rt, P, fl, true);
     if (use_floor) {
       int rt2, P2;
       floor_plan(max_q, nd, rt2, P2);
@@ -3127,9 +3226,10 @@ int64_t fwav_debug_topk_qb(int geo) { return geo >= 0 && geo <= 3 ? geometry_qb(
 int fwav_debug_sim_topk_layout(int64_t max_q, int64_t nd, int64_t* offsets) {
   FWAV_CHECK_ARG(max_q >= 0 && nd > 0 && offsets, FWAV_ERR_ARG, "fwav_debug_sim_topk_layout: bad args");
   const TopkLayout L = topk_layout(max_q > 0 ? max_q : 1, nd);
-  const size_t v[15] = {L.keys, L.share, L.ovf2, L.n_ovf2, L.seeds2, L.ovf1, L.n_ovf1, L.seeds1,
-                        L.miss, L.n_miss, L.miss2, L.n_miss2, L.floor_key, L.pilot, L.total};
-  for (int i = 0; i < 15; ++i) offsets[i] = (int64_t)v[i];
+  const size_t v[19] = {L.keys,      L.share, L.ovf2,    L.n_ovf2,     L.seeds2,     L.ovf1,  L.n_ovf1,
+                        L.seeds1,    L.miss,  L.n_miss,  L.miss2,      L.n_miss2,    L.floor_key, L.order,
+                        L.n_order,   L.order_bits,       L.order_bsum, L.pilot,      L.total};
+  for (int i = 0; i < 19; ++i) offsets[i] = (int64_t)v[i];
   return FWAV_OK;
 }
 

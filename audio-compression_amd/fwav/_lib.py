@@ -196,7 +196,7 @@ def size_call(name: str, *args) -> int:
 
 #: fwav_debug_sim_topk_layout's regions, in its order
 SIM_TOPK_LAYOUT = ("keys", "share", "ovf2", "n_ovf2", "seeds2", "ovf1", "n_ovf1", "seeds1", "miss", "n_miss", "miss2",
-                   "n_miss2", "floor_key", "pilot", "total")
+                   "n_miss2", "floor_key", "order", "n_order", "order_bits", "order_bsum", "pilot", "total")
 
 
 def sim_topk_layout(max_q: int, n_domains: int) -> dict:

@@ -58,14 +58,15 @@ int64_t fwav_debug_topk_qb(int geo);
  * the default rank, with the second pass's floor `value` (≥ 0) below the pilots' smallest estimate instead of 0.15.
  * All return the same candidates. */
 int fwav_debug_topk_floor(int mode, float value);
-/* Diagnostic override of the floor's second pass: table pieces per split block of misses (1 … 32; 0 = the default:
- * 32 below 131,072 queries, else 16).  Re-query fwav_sim_topk_workspace_size afterwards.  All return the same
- * candidates. */
+/* Diagnostic override of the floor's second pass: table pieces per split block of misses (1 … 64; 0 = the default:
+ * the most of 64 / 32 / 16 with which the expected misses fill one round of workgroups).  Re-query
+ * fwav_sim_topk_workspace_size afterwards.  All return the same candidates. */
 int fwav_debug_topk_floor_pieces(int pieces);
 /* Byte offsets of the fp16 search's workspace regions (K <= 64) for max_q queries over n_domains domains, as this
- * library lays them out: offsets[0..14] = keys, share, ovf2, n_ovf2, seeds2, ovf1, n_ovf1, seeds1, miss, n_miss, miss2,
- * n_miss2, floor_key, pilot, total (= fwav_sim_topk_workspace_size).  Every region before `pilot` sits at the same
- * offset in libfwav.so; the product library adds the pilots' scores only where its floor can run. */
+ * library lays them out: offsets[0..18] = keys, share, ovf2, n_ovf2, seeds2, ovf1, n_ovf1, seeds1, miss, n_miss, miss2,
+ * n_miss2, floor_key, order, n_order, order_bits, order_bsum (the search's ascending copy of the active list and its
+ * bitmap), pilot, total (= fwav_sim_topk_workspace_size).  Every region before `pilot` sits at the same offset in
+ * libfwav.so; the product library adds the pilots' scores only where its floor can run. */
 int fwav_debug_sim_topk_layout(int64_t max_q, int64_t n_domains, int64_t* offsets);
 
 #ifdef __cplusplus

@@ -1,6 +1,7 @@
 """Counters of the fp16 search's first pass (STATS build of the kernel: replayed chunks, firing tiles, appends,
 compactions, time shares) on cfg2 for the first AB_NQ queries (tools only).
-usage: AB_NQ=41344 python tools/first_stats.py   (AB_DBG=262144: the product's geometry instead of the base; 786432: and its floor)"""
+usage: AB_NQ=41344 python tools/first_stats.py   (AB_DBG=262144: the product's geometry instead of the base; 786432: and its floor; AB_RUNS=1: the active
+list in runs of 64 in random order, as fwav_prune leaves it)"""
 import os as _os_dbg
 _os_dbg.environ.setdefault("FWAV_DEBUG_LIBRARY", "1")  # the search knobs: libfwav_debug.so
 import os
@@ -40,6 +41,10 @@ if os.environ.get("AB_PLAN"):  # "rt,pieces": the work-plan override (fwav_debug
     call("fwav_debug_topk_plan", *[int(x) for x in os.environ["AB_PLAN"].split(",")])
 nq = int(os.environ.get("AB_NQ", nr))
 active = torch.arange(nq, dtype=torch.int32, device="cuda")
+if os.environ.get("AB_RUNS") == "1":  # fwav_prune's order: runs of 64 consecutive ranges in a random run order
+    _g = torch.Generator().manual_seed(0)
+    active = torch.cat([torch.arange(r * 64, min(nq, r * 64 + 64), dtype=torch.int32)
+                        for r in torch.randperm((nq + 63) // 64, generator=_g).tolist()]).cuda()
 n_active = torch.tensor([nq], dtype=torch.int32, device="cuda")
 wsn = size_call("fwav_sim_topk_workspace_size", nq, nd, 64)
 wsk = torch.empty(wsn, dtype=torch.uint8, device="cuda")
