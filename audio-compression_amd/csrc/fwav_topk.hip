@@ -50,7 +50,7 @@
     defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
     defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || \
     defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE) || \
-    defined(FWAV_FLOOR_PILOTS) || defined(FWAV_FLOOR_RANK))
+    defined(FWAV_FLOOR_PILOTS) || defined(FWAV_FLOOR_RANK) || defined(FWAV_TOPK_YOUNG))
 #error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
 #endif
 
@@ -544,6 +544,7 @@ static_assert(kPlanMaxPieces <= kMaxPieces, "first-pass plans stay within the me
 struct TopkPlan {
   int64_t nb, F, R;
   int P, qb;
+  int young;  // one-round plans: the first table piece whose items share their CU as its younger workgroup (0: none)
   bool halves, pm;
   __host__ __device__ int64_t items() const { return F + R * P; }
   // the item of table piece p of split block b
@@ -574,16 +575,37 @@ __device__ __forceinline__ bool floor_miss(uint32_t fkey, const FloorCtl& fl, in
   if (miss && (threadIdx.x & 63) == 0) fl.miss[atomicAdd(fl.n_miss, 1)] = qid;
   return miss;
 }
+// P: table pieces per split block, −1 for query halves; bits 8 and up: TopkPlan::young (plan_young)
 __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, int qb) {
   TopkPlan pl;
   pl.qb = qb;
   pl.nb = cdiv(n_queries > 0 ? n_queries : 0, qb);
+  pl.young = P > 0 ? (P >> 8) : 0;
+  P = P > 0 ? (P & 0xFF) : P;
   pl.halves = P < 0;
   pl.P = pl.halves ? 2 : (P < 1 ? 1 : (P > kMaxPieces ? kMaxPieces : P));
   pl.R = pl.P == 1 ? 0 : (pl.nb < rt ? pl.nb : (int64_t)rt);
   pl.F = pl.nb - pl.R;
   pl.pm = FWAV_TOPK_PMAJOR && !pl.halves && pl.P > 1 && pl.R > 0;
   return pl;
+}
+// Chunk range [c0, c1) of table piece `piece` of `np`.  Even, unless the plan is one round of workgroups two to a CU
+// (TopkPlan::young): a CU's younger workgroup loses the issue arbitration to its older one (oldest-first) and ran
+// its piece 13 % longer (41,344 queries, pieces 3–5 vs 0–2: 1.95 vs 1.72 ms median, tools/topk_timeline.py TL_R,
+// profiles/r06/timeline_pieces_eighth.log), so the older pieces take 17 / 16 of the mean and the younger 15 / 16.
+constexpr int kOldWeight = 17, kYoungWeight = 15;
+__host__ __device__ inline void piece_chunks(const TopkPlan& pl, int piece, int np, int nchunks, int& c0, int& c1) {
+  if (pl.young <= 0 || pl.young >= np || np != pl.P) {
+    c0 = (int)((int64_t)nchunks * piece / np);
+    c1 = (int)((int64_t)nchunks * (piece + 1) / np);
+    return;
+  }
+  auto cum = [&](int p) -> int64_t {
+    return p <= pl.young ? (int64_t)p * kOldWeight : (int64_t)pl.young * kOldWeight + (int64_t)(p - pl.young) * kYoungWeight;
+  };
+  const int64_t tot = cum(np);
+  c0 = (int)((int64_t)nchunks * cum(piece) / tot);
+  c1 = (int)((int64_t)nchunks * cum(piece + 1) / tot);
 }
 // Query (position in the active list) of slot ql = group·32 + col of query block `block`.  INTERLEAVE: a block's
 // query groups come from different regions of the list (group g of block b is query group g·nb + b), so every block
@@ -1638,7 +1660,8 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   const int nchunks = (int)cdiv(nd, kChunk);  // < 2^31 / 256: chunk arithmetic stays 32-bit (scalar)
   if ((FWAV_TOPK_PRIO & 1) && wave >= W / 2) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half
   // this item's chunk range [c0, c1) (the whole table unless the block is split)
-  const int c0 = (int)((int64_t)nchunks * piece / npieces), c1 = (int)((int64_t)nchunks * (piece + 1) / npieces);
+  int c0, c1;
+  piece_chunks(plan, piece, npieces, nchunks, c0, c1);
   const int ngroups = (c1 - c0 + G - 1) / G;
   const u32x4* src = reinterpret_cast<const u32x4*>(emb16);
   // Chunk stream: global → LDS directly (global_load_lds_dwordx4: no staging registers, no ds_write).  The
@@ -2315,6 +2338,9 @@ constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2, kGeoCentWide = 3;
 #ifndef FWAV_TOPK_CPDBL
 #define FWAV_TOPK_CPDBL 4  // centroid geometry, blocks on at most half the slots: pieces doubled below this count
 #endif
+#ifndef FWAV_TOPK_YOUNG
+#define FWAV_TOPK_YOUNG 1  // one-round plans: smaller table pieces for the CUs' younger workgroups (piece_chunks)
+#endif
 #ifndef FWAV_TOPK_CENTWIDE
 // tables past the Infinity Cache: the centroid filter in the wide geometry (16 waves × 2 sets of 32, 8-chunk groups,
 // one workgroup per CU).  A cfg4 shard (337,500 queries × 86.4 M domains, hi/lo band, identical outputs): wide
@@ -2443,6 +2469,24 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P, i
   // every piece streams at least 16 chunks (4,096 domains)
   const int64_t pmax = cdiv(nd, kChunk) / 16;
   if (P > pmax) P = (int)(pmax > 1 ? pmax : 1);
+  // one round of split blocks, two workgroups to a CU: the pieces whose items start in the round's second half run as
+  // their CU's younger workgroup and get the smaller share of the table (piece_chunks)
+  if (g_plan_rt < 0 && P > 1 && P <= 0xFF) {
+    int cus, per_cu;
+    topk_device_slots(geo, cus, per_cu);
+    const int64_t slots = (int64_t)cus * per_cu;
+    const int64_t nb = cdiv(max_q > 0 ? max_q : 1, geometry_qb(geo));
+    const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(geo));
+    if (FWAV_TOPK_YOUNG && per_cu == 2 && pl.F == 0 && pl.R == nb && pl.pm && pl.items() <= slots &&
+        2 * pl.items() > slots) {
+      // the first piece whose items start past slots / 2 — only where a piece boundary falls near it (one rank's
+      // eighth of cfg2: 81 blocks × 6 pieces, boundary at item 243 of 256: 2.56 → 2.53 ms; a quarter, 162 × 3,
+      // boundary at 324: 4.34 → 4.38 with the skew, so it keeps the even split; profiles/r06/ab_young.log)
+      const int64_t y = (slots / 2 + pl.R / 2) / pl.R;
+      const int64_t off = y * pl.R - slots / 2;
+      if (y > 0 && y < P && 4 * (off < 0 ? -off : off) <= pl.R) P |= (int)(y << 8);
+    }
+  }
 }
 // ---------------------------------------------------------------------------------------- speculative floor
 // A first pass of at least kFloorMinQ queries over at least kFloorMinD domains starts every band

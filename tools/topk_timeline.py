@@ -70,3 +70,11 @@ for i in order:
 first = s < 50.0
 print(f"first-round workgroups {int(first.sum())}: median duration {np.median((e - s)[first]) / 1000:.2f} ms; "
       f"later {int((~first).sum())}: median {np.median((e - s)[~first]) / 1000:.2f} ms")
+if os.environ.get("TL_R"):  # piece-major plan with R split blocks from item 0: median duration per table piece
+    R = int(os.environ["TL_R"])
+    dur = (e - s) / 1000
+    for p in range(int(ids.max()) // R + 1):
+        sel = (ids // R) == p
+        if sel.any():
+            print(f"piece {p}: {int(sel.sum())} items, duration median {np.median(dur[sel]):.2f} ms, "
+                  f"max {dur[sel].max():.2f}")
