@@ -50,7 +50,7 @@
     defined(FWAV_TOPK_MAXP) || defined(FWAV_TOPK_PMAJOR) || defined(FWAV_TOPK_PRIO) || defined(FWAV_TOPK_QS) || \
     defined(FWAV_TOPK_RB) || defined(FWAV_TOPK_SEEDHALF) || defined(FWAV_TOPK_SMALLSORT) || defined(FWAV_TOPK_W) || \
     defined(FWAV_TOPK_WARM) || defined(FWAV_TOPK_WIDE_MIN) || defined(FWAV_TOPK_WIN) || defined(FWAV_TOPK_WPE) || \
-    defined(FWAV_FLOOR_PILOTS) || defined(FWAV_FLOOR_RANK) || defined(FWAV_TOPK_YOUNG))
+    defined(FWAV_FLOOR_PILOTS) || defined(FWAV_FLOOR_RANK) || defined(FWAV_TOPK_YOUNG) || defined(FWAV_TOPK_TAIL))
 #error "experiment switches build the debug library only (-DFWAV_DEBUG_API)"
 #endif
 
@@ -541,10 +541,12 @@ static_assert(kPlanMaxPieces <= kMaxPieces, "first-pass plans stay within the me
 #ifndef FWAV_TOPK_PMAJOR
 #define FWAV_TOPK_PMAJOR 1
 #endif
+constexpr int kOldWeight = 17, kYoungWeight = 15;  // piece_chunks: a CU's older / younger workgroup
 struct TopkPlan {
   int64_t nb, F, R;
   int P, qb;
-  int young;  // one-round plans: the first table piece whose items share their CU as its younger workgroup (0: none)
+  // two-class table split (piece_chunks): pieces [0, young) weigh wa, [young, P) wb (young 0: an even split)
+  int young, wa, wb;
   bool halves, pm;
   __host__ __device__ int64_t items() const { return F + R * P; }
   // the item of table piece p of split block b
@@ -580,7 +582,13 @@ __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, 
   TopkPlan pl;
   pl.qb = qb;
   pl.nb = cdiv(n_queries > 0 ? n_queries : 0, qb);
-  pl.young = P > 0 ? (P >> 8) : 0;
+  pl.young = P > 0 ? ((P >> 8) & 0xFF) : 0;
+  pl.wb = P > 0 ? ((P >> 16) & 0x1F) : 0;  // bits 16–20 / 21–25: the weights (0: the younger-workgroup pair)
+  pl.wa = P > 0 ? ((P >> 21) & 0x1F) : 0;
+  if (pl.wa == 0 || pl.wb == 0) {
+    pl.wa = kOldWeight;
+    pl.wb = kYoungWeight;
+  }
   P = P > 0 ? (P & 0xFF) : P;
   pl.halves = P < 0;
   pl.P = pl.halves ? 2 : (P < 1 ? 1 : (P > kMaxPieces ? kMaxPieces : P));
@@ -593,7 +601,6 @@ __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, 
 // (TopkPlan::young): a CU's younger workgroup loses the issue arbitration to its older one (oldest-first) and ran
 // its piece 13 % longer (41,344 queries, pieces 3–5 vs 0–2: 1.95 vs 1.72 ms median, tools/topk_timeline.py TL_R,
 // profiles/r06/timeline_pieces_eighth.log), so the older pieces take 17 / 16 of the mean and the younger 15 / 16.
-constexpr int kOldWeight = 17, kYoungWeight = 15;
 __host__ __device__ inline void piece_chunks(const TopkPlan& pl, int piece, int np, int nchunks, int& c0, int& c1) {
   if (pl.young <= 0 || pl.young >= np || np != pl.P) {
     c0 = (int)((int64_t)nchunks * piece / np);
@@ -601,7 +608,7 @@ __host__ __device__ inline void piece_chunks(const TopkPlan& pl, int piece, int 
     return;
   }
   auto cum = [&](int p) -> int64_t {
-    return p <= pl.young ? (int64_t)p * kOldWeight : (int64_t)pl.young * kOldWeight + (int64_t)(p - pl.young) * kYoungWeight;
+    return p <= pl.young ? (int64_t)p * pl.wa : (int64_t)pl.young * pl.wa + (int64_t)(p - pl.young) * pl.wb;
   };
   const int64_t tot = cum(np);
   c0 = (int)((int64_t)nchunks * cum(piece) / tot);
@@ -2300,8 +2307,10 @@ __device__ __forceinline__ void merge_query(const TopkPlan& plan, int64_t w, int
 // Host-side plan: default policy from the device's workgroup slots, or a diagnostic override.
 #ifdef FWAV_DEBUG_API
 static int g_plan_rt = -1, g_plan_p = -1;  // fwav_debug_topk_plan (debug library only)
+static int g_tail_wb = -1;  // fwav_debug_topk_tail (debug library only): the last piece's weight in 1/16
 #else
 constexpr int g_plan_rt = -1, g_plan_p = -1;
+constexpr int g_tail_wb = -1;
 #endif
 // Per-device caches (the caller makes the stream's device current: fwav.engine wraps every call in
 // torch.cuda.device); kMaxDev bounds the device ordinal.
@@ -2337,6 +2346,9 @@ constexpr int g_wide = -1;
 constexpr int kGeoBase = 0, kGeoWide = 1, kGeoCent = 2, kGeoCentWide = 3;
 #ifndef FWAV_TOPK_CPDBL
 #define FWAV_TOPK_CPDBL 4  // centroid geometry, blocks on at most half the slots: pieces doubled below this count
+#endif
+#ifndef FWAV_TOPK_TAIL
+#define FWAV_TOPK_TAIL 12  // multi-round plans of split blocks: the last piece's table share in 1/16 (16, 0: even)
 #endif
 #ifndef FWAV_TOPK_YOUNG
 #define FWAV_TOPK_YOUNG 1  // one-round plans: smaller table pieces for the CUs' younger workgroups (piece_chunks)
@@ -2472,6 +2484,7 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P, i
   // one round of split blocks, two workgroups to a CU: the pieces whose items start in the round's second half run as
   // their CU's younger workgroup and get the smaller share of the table (piece_chunks)
   if (g_plan_rt < 0 && P > 1 && P <= 0xFF) {
+    const int tail_wb = g_tail_wb >= 0 ? g_tail_wb : FWAV_TOPK_TAIL;
     int cus, per_cu;
     topk_device_slots(geo, cus, per_cu);
     const int64_t slots = (int64_t)cus * per_cu;
@@ -2485,6 +2498,13 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P, i
       const int64_t y = (slots / 2 + pl.R / 2) / pl.R;
       const int64_t off = y * pl.R - slots / 2;
       if (y > 0 && y < P && 4 * (off < 0 ? -off : off) <= pl.R) P |= (int)(y << 8);
+    } else if (tail_wb > 0 && tail_wb != 16 && pl.F == 0 && pl.R == nb && pl.pm && pl.items() > slots) {
+      // several rounds of split blocks, piece-major: the items that start last are the blocks' last pieces, and the
+      // launch ends with the slowest of them, so the last piece of every block takes tail_wb / 16 of the others'
+      // share of the table.  Same process (tools/diag/topk_reps.py, FWAV_DEBUG_TOPK_TAIL, profiles/r06/tail_sweep.log):
+      // cfg2 (646 centroid blocks × 3 pieces) 14.26–14.46 ms even, 13.98 / 14.02–14.06 / 14.16 / 14.22 at 11 / 12 /
+      // 13 / 14; 165,375 queries 7.72 → 7.57 at 12
+      P |= ((P - 1) << 8) | (tail_wb << 16) | (16 << 21);
     }
   }
 }
@@ -3279,6 +3299,12 @@ int fwav_debug_sim_topk_layout(int64_t max_q, int64_t nd, int64_t* offsets) {
 
 // Diagnostic override of the fp16 search's work plan (rt < 0: default policy).  Re-query
 // fwav_sim_topk_workspace_size after changing it.
+int fwav_debug_topk_tail(int wb) {
+  FWAV_CHECK_ARG(wb >= -1 && wb <= 31, FWAV_ERR_ARG, "fwav_debug_topk_tail: weight outside [-1, 31]");
+  g_tail_wb = wb;
+  return FWAV_OK;
+}
+
 int fwav_debug_topk_plan(int rt, int pieces) {
   FWAV_CHECK_ARG(pieces == -1 || (pieces >= 1 && pieces <= kMaxPieces), FWAV_ERR_ARG,
                  "fwav_debug_topk_plan: pieces outside [1, %d] (or -1: query halves)", kMaxPieces);

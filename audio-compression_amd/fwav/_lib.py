@@ -71,6 +71,7 @@ SIGNATURES = {
 DEBUG_SIGNATURES = {
     "fwav_debug_sim_topk": (I32, [P, P, I64, P, P, I64, I64, I32, P, P, SZ, I32, P, P]),
     "fwav_debug_topk_plan": (I32, [I32, I32]),
+    "fwav_debug_topk_tail": (I32, [I32]),
     "fwav_debug_topk_plan_cover": (I32, [I64, I32, I32, I32, P, P]),
     "fwav_debug_topk_mode": (I32, [I32]),
     "fwav_debug_topk_geometry": (I32, [I32]),
@@ -145,6 +146,8 @@ def debug_lib() -> C.CDLL:
             _libs["debug"].fwav_debug_topk_floor(int(mode), float(value or 0.0))
         if os.environ.get("FWAV_DEBUG_TOPK_GEOMETRY"):
             _libs["debug"].fwav_debug_topk_geometry(int(os.environ["FWAV_DEBUG_TOPK_GEOMETRY"]))
+        if os.environ.get("FWAV_DEBUG_TOPK_TAIL"):
+            _libs["debug"].fwav_debug_topk_tail(int(os.environ["FWAV_DEBUG_TOPK_TAIL"]))
         if os.environ.get("FWAV_DEBUG_TOPK_P2"):
             _libs["debug"].fwav_debug_topk_floor_pieces(int(os.environ["FWAV_DEBUG_TOPK_P2"]))
     return _libs["debug"]
@@ -177,6 +180,7 @@ class debug_library:
         d.fwav_debug_topk_geometry(-1)
         d.fwav_debug_topk_floor(-1, 0.0)
         d.fwav_debug_topk_floor_pieces(0)
+        d.fwav_debug_topk_tail(-1)
         _active = self.prev
         return False
 

@@ -27,6 +27,9 @@ int fwav_debug_sim_topk(const float* emb, const void* emb16, int64_t n_domains, 
  * ranges, or with pieces == -1 into two query halves (rt < 0 restores the default policy).  Every plan returns the
  * same candidates.  Re-query fwav_sim_topk_workspace_size afterwards. */
 int fwav_debug_topk_plan(int rt, int pieces);
+/* Diagnostic: in multi-round plans whose blocks are all split, the last table piece of every block takes wb / 16 of
+ * the other pieces' share (0 or 16: an even split; −1: the default, 12).  Same candidates. */
+int fwav_debug_topk_tail(int wb);
 /* The first pass fwav_sim_topk would launch for max_q queries over n_domains domains on the current device (host
  * only): info[0] = geometry (0 = base, 1 = wide, 2 = centroid, 3 = centroid wide), info[1] = first-pass mode (0 = fp16 band, 1 = hi/lo band), info[2] = table
  * pieces per split block (−1: query halves); blocks[0] = whole-table blocks, blocks[1] = split blocks,
