@@ -3038,11 +3038,20 @@ static int launch_topk(const float* emb, const _Float16* emb16, int64_t nd, cons
     // Speculative floor (FloorCtl): from the exact scores of kFloorPilots evenly spaced queries against every
     // (K/8)-th domain (k_floor_pilot), a guess at the lowest K-th score of the search; the queries it may cut are
     // searched again at a lower floor, and the few that one cuts without any (base geometry, table pieces).
-    // the search's own ascending copy of the caller's active list (order_active): every pass below reads it
-    int32_t* const order = reinterpret_cast<int32_t*>(wb + lay.order);
-    int32_t* const n_order = reinterpret_cast<int32_t*>(wb + lay.n_order);
-    order_active(active, n_active, max_q, reinterpret_cast<uint32_t*>(wb + lay.order_bits),
-                 reinterpret_cast<uint32_t*>(wb + lay.order_bsum), order, n_order, st);
+    // the centroid geometry's passes on the search's own ascending copy of the caller's active list (order_active;
+    // every pass below reads it), where it was measured; the other geometries on the caller's order (ascending ids
+    // are not better everywhere: cfg3's sliced search on ascending slices ran 373 instead of 347 ms per step,
+    // profiles/r06/active_order/cfg3_*.log)
+    const int32_t* order = active;
+    const int32_t* n_order = n_active;
+    if (geo == kGeoCent) {
+      int32_t* const ord = reinterpret_cast<int32_t*>(wb + lay.order);
+      int32_t* const n_ord = reinterpret_cast<int32_t*>(wb + lay.n_order);
+      order_active(active, n_active, max_q, reinterpret_cast<uint32_t*>(wb + lay.order_bits),
+                   reinterpret_cast<uint32_t*>(wb + lay.order_bsum), ord, n_ord, st);
+      order = ord;
+      n_order = n_ord;
+    }
     const int fmode = floor_mode();
     // (counter launches run without the floor unless dbg bit 19 asks for the product's floor too)
     const bool use_floor = (!stats_first || (dbg & (1 << 19))) && K <= 64 && floor_by_default(max_q, nd);

@@ -407,12 +407,6 @@ def _search_sub_blocks(nsub, m, nd, k, lo, rs, threads, sc, tie_order, emb, emb1
     slices' tie records as one list."""
     dev = rsh.device
     bounds = _slice_bounds(m, nsub)
-    if nsub > 1:
-        # ascending ids in every slice: fwav_prune lists its ranges in runs of 64 in atomic order, and the search only
-        # reorders a list whose ids lie below its own query count (a slice's do not) — the first pass runs faster on
-        # ascending ids (DESIGN §3.1); entries past n_active sort last
-        pos = torch.arange(active.numel(), dtype=torch.int32, device=dev)
-        active = torch.where(pos < n_active, active, torch.full_like(active, 2**31 - 1)).sort().values
     wk = max(size_call("fwav_sim_topk_workspace_size", b - a, nd, k) for a, b in bounds) \
         if (emb16 is not None or k > 64) else 0
     wsk = torch.empty(max(wk, 16), dtype=torch.uint8, device=dev)
