@@ -3275,6 +3275,21 @@ int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t*
 // The first pass fwav_sim_topk would launch for max_q queries over nd domains on the current device (no launch):
 // geometry (1 = wide), first-pass mode (0 = S16, 1 = HL), whole-table blocks F, split blocks R, pieces P (−1: query
 // halves), grid.
+// The default first-pass plan's chunk range of every table piece (piece_chunks, with the floor as the launch would
+// decide it): c01[2p], c01[2p + 1] = [c0, c1) of piece p < *np (at most kMaxPieces); *np = 1 for an unsplit plan.
+int fwav_debug_topk_piece_chunks(int64_t max_q, int64_t nd, int32_t* c01, int32_t* np) {
+  FWAV_CHECK_ARG(max_q > 0 && nd > 0 && c01 && np, FWAV_ERR_ARG, "fwav_debug_topk_piece_chunks: bad args");
+  const int geo = first_geometry(nd, max_q);
+  int rt, P;
+  host_plan_for(max_q, nd, geo, rt, P);
+  const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(geo));
+  const int n = pl.halves || pl.R == 0 ? 1 : pl.P;
+  const int nchunks = (int)cdiv(nd, kChunk);
+  for (int p = 0; p < n; ++p) piece_chunks(pl, p, n, nchunks, c01[2 * p], c01[2 * p + 1]);
+  *np = n;
+  return FWAV_OK;
+}
+
 int fwav_debug_topk_plan_info(int64_t max_q, int64_t nd, int32_t* info, int64_t* blocks) {
   FWAV_CHECK_ARG(max_q >= 0 && nd > 0 && info && blocks, FWAV_ERR_ARG, "fwav_debug_topk_plan_info: bad args");
   const int geo = first_geometry(nd, max_q);

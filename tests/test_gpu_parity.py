@@ -307,6 +307,67 @@ def test_overflow_with_sparse_active_list(first_mode):
     assert np.array_equal(out[0], out[1])
 
 
+def test_active_list_order_does_not_change_candidates():
+    """The centroid geometry searches its own ascending copy of the active list (order_active): the same
+    41,344 queries listed ascending, in fwav_prune's kind of order (runs of 64 in random run order), descending, and
+    with every id listed twice (duplicates collapse) give the same candidate rows — and those of the all-f32 kernel —
+    with the workspace untouched past its end; a list holding an id past max_q is searched as given."""
+    from fwav import engine as E
+    from fwav import synth
+    from fwav._lib import size_call
+    sig = td(synth.noise(60.0, 44100, seed=3))
+    tile, K = 2048, 64
+    rs, step = E.geometry(tile)
+    nd = (sig.numel() - tile) // step + 1
+    st = torch.cuda.current_stream().cuda_stream
+    tab = E.embed_tables(rs, sig.device)
+    pool = torch.empty(nd * rs, device=sig.device)
+    emb = torch.empty(nd * 16, device=sig.device)
+    emb16 = torch.empty(2 * ((nd + 255) // 256) * 256 * 16, dtype=torch.float16, device=sig.device)
+    ws = torch.empty(max(size_call("fwav_pool_workspace_size", sig.numel(), tile, rs, step), 16), dtype=torch.uint8,
+                     device=sig.device)
+    call("fwav_pool_embed", sig.data_ptr(), sig.numel(), tile, rs, step, tab.data_ptr(), pool.data_ptr(),
+         emb.data_ptr(), emb16.data_ptr(), ws.data_ptr(), ws.numel(), st)
+    nq = 41_344
+    lo = 100_000
+    g = torch.Generator().manual_seed(1)
+    runs = torch.randperm((nq + 63) // 64, generator=g).tolist()
+    asc = torch.arange(nq, dtype=torch.int32)
+    lists = {"ascending": asc,
+             "runs": torch.cat([asc[r * 64:(r + 1) * 64] for r in runs]),
+             "descending": asc.flip(0),
+             "duplicates": torch.cat([asc, asc])}
+    out = {}
+    for name, lst in lists.items():
+        for e16 in ((emb16.data_ptr(),) if name != "ascending" else (emb16.data_ptr(), None)):
+            act = lst.to(sig.device)
+            max_q = act.numel()
+            n_act = torch.tensor([max_q], dtype=torch.int32, device=sig.device)
+            wsn = size_call("fwav_sim_topk_workspace_size", max_q, nd, K)
+            guard = 1 << 20
+            wsk = torch.zeros(wsn + guard, dtype=torch.uint8, device=sig.device)
+            cand = torch.full((max_q * K,), -7, dtype=torch.int32, device=sig.device)
+            call("fwav_sim_topk", emb.data_ptr(), e16, nd, act.data_ptr(), n_act.data_ptr(), max_q, lo, K, 16,
+                 cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
+            torch.cuda.synchronize()
+            assert int(wsk[wsn:].count_nonzero().item()) == 0, f"{name}: write past the workspace"
+            out[(name, e16 is None)] = cand.view(max_q, K)[:nq].cpu().numpy()
+    ref = out[("ascending", True)]  # the all-f32 kernel
+    for key, c in out.items():
+        assert np.array_equal(c, ref), key
+    # ids past max_q (33,344 ≥ 32,768 listed: the centroid geometry): the list is searched as given
+    act = torch.arange(8_000, nq, dtype=torch.int32, device=sig.device).flip(0)
+    max_q = act.numel()
+    n_act = torch.tensor([max_q], dtype=torch.int32, device=sig.device)
+    wsn = size_call("fwav_sim_topk_workspace_size", max_q, nd, K)
+    wsk = torch.zeros(wsn, dtype=torch.uint8, device=sig.device)
+    cand = torch.full((nq * K,), -7, dtype=torch.int32, device=sig.device)
+    call("fwav_sim_topk", emb.data_ptr(), emb16.data_ptr(), nd, act.data_ptr(), n_act.data_ptr(), max_q, lo, K, 16,
+         cand.data_ptr(), None, wsk.data_ptr(), wsn, st)
+    torch.cuda.synchronize()
+    assert np.array_equal(cand.view(nq, K)[8_000:].cpu().numpy(), ref[8_000:])
+
+
 @pytest.mark.parametrize("n", [1, 7, 8, 127, 128, 129, 8191, 8192, 8193, 100_003, 2_646_000])
 def test_weighted_energy_is_numpy_f32_sum(n):
     """The silent-input test's Σ x² (fractal.py:1083) equals np.sum(x ** 2) on float32 bit-for-bit."""
