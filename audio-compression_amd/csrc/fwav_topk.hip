@@ -547,6 +547,9 @@ struct TopkPlan {
   int P, qb;
   // two-class table split (piece_chunks): pieces [0, young) weigh wa, [young, P) wb (young 0: an even split)
   int young, wa, wb;
+  // one-round plans (bit 30 of P): the first item index that starts as its CU's younger workgroup (0: none); each
+  // block's pieces weigh kOldWeight / kYoungWeight by their own items' side of it
+  int ybound;
   bool halves, pm;
   __host__ __device__ int64_t items() const { return F + R * P; }
   // the item of table piece p of split block b
@@ -582,9 +585,11 @@ __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, 
   TopkPlan pl;
   pl.qb = qb;
   pl.nb = cdiv(n_queries > 0 ? n_queries : 0, qb);
-  pl.young = P > 0 ? ((P >> 8) & 0xFF) : 0;
-  pl.wb = P > 0 ? ((P >> 16) & 0x1F) : 0;  // bits 16–20 / 21–25: the weights (0: the younger-workgroup pair)
-  pl.wa = P > 0 ? ((P >> 21) & 0x1F) : 0;
+  const bool by_item = P > 0 && ((P >> 30) & 1);
+  pl.ybound = by_item ? ((P >> 8) & 0xFFF) : 0;  // bits 8–19
+  pl.young = P > 0 && !by_item ? ((P >> 8) & 0xFF) : 0;
+  pl.wb = P > 0 && !by_item ? ((P >> 16) & 0x1F) : 0;  // bits 16–20 / 21–25: the weights (0: the younger pair)
+  pl.wa = P > 0 && !by_item ? ((P >> 21) & 0x1F) : 0;
   if (pl.wa == 0 || pl.wb == 0) {
     pl.wa = kOldWeight;
     pl.wb = kYoungWeight;
@@ -601,7 +606,21 @@ __host__ __device__ inline TopkPlan make_plan(int64_t n_queries, int rt, int P, 
 // (TopkPlan::young): a CU's younger workgroup loses the issue arbitration to its older one (oldest-first) and ran
 // its piece 13 % longer (41,344 queries, pieces 3–5 vs 0–2: 1.95 vs 1.72 ms median, tools/topk_timeline.py TL_R,
 // profiles/r06/timeline_pieces_eighth.log), so the older pieces take 17 / 16 of the mean and the younger 15 / 16.
-__host__ __device__ inline void piece_chunks(const TopkPlan& pl, int piece, int np, int nchunks, int& c0, int& c1) {
+__host__ __device__ inline void piece_chunks(const TopkPlan& pl, int64_t block, int piece, int np, int nchunks, int& c0,
+                                             int& c1) {
+  if (pl.ybound > 0 && np == pl.P && block >= pl.F) {
+    // by each piece's own item: older (item < ybound) kOldWeight, younger kYoungWeight
+    int64_t a = 0, tot = 0;
+    for (int p = 0; p < np; ++p) {
+      const int w = pl.item_of(block, p) < pl.ybound ? kOldWeight : kYoungWeight;
+      if (p < piece) a += w;
+      tot += w;
+    }
+    const int w = pl.item_of(block, piece) < pl.ybound ? kOldWeight : kYoungWeight;
+    c0 = (int)((int64_t)nchunks * a / tot);
+    c1 = (int)((int64_t)nchunks * (a + w) / tot);
+    return;
+  }
   if (pl.young <= 0 || pl.young >= np || np != pl.P) {
     c0 = (int)((int64_t)nchunks * piece / np);
     c1 = (int)((int64_t)nchunks * (piece + 1) / np);
@@ -1668,7 +1687,7 @@ __global__ __launch_bounds__(64 * W, MODE == kModeEX ? FWAV_TOPK_EXWPE : (CENT ?
   if ((FWAV_TOPK_PRIO & 1) && wave >= W / 2) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half
   // this item's chunk range [c0, c1) (the whole table unless the block is split)
   int c0, c1;
-  piece_chunks(plan, piece, npieces, nchunks, c0, c1);
+  piece_chunks(plan, block, piece, npieces, nchunks, c0, c1);
   const int ngroups = (c1 - c0 + G - 1) / G;
   const u32x4* src = reinterpret_cast<const u32x4*>(emb16);
   // Chunk stream: global → LDS directly (global_load_lds_dwordx4: no staging registers, no ds_write).  The
@@ -2492,12 +2511,10 @@ static void host_plan_for(int64_t max_q, int64_t nd, int geo, int& rt, int& P, i
     const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(geo));
     if (FWAV_TOPK_YOUNG && per_cu == 2 && pl.F == 0 && pl.R == nb && pl.pm && pl.items() <= slots &&
         2 * pl.items() > slots) {
-      // the first piece whose items start past slots / 2 — only where a piece boundary falls near it (one rank's
-      // eighth of cfg2: 81 blocks × 6 pieces, boundary at item 243 of 256: 2.56 → 2.53 ms; a quarter, 162 × 3,
-      // boundary at 324: 4.34 → 4.38 with the skew, so it keeps the even split; profiles/r06/ab_young.log)
-      const int64_t y = (slots / 2 + pl.R / 2) / pl.R;
-      const int64_t off = y * pl.R - slots / 2;
-      if (y > 0 && y < P && 4 * (off < 0 ? -off : off) <= pl.R) P |= (int)(y << 8);
+      // every block's pieces weighed by their own items' side of slots / 2 (TopkPlan::ybound).  (Round 6 first
+      // weighed whole pieces, from the first piece past slots / 2 on: one rank's eighth of cfg2, 81 blocks × 6
+      // pieces in one round, 2.56 → 2.53 ms, profiles/r06/ab_young.log)
+      if (slots / 2 < 0xFFF) P |= (1 << 30) | (int)((slots / 2) << 8);
     } else if (tail_wb > 0 && tail_wb != 16 && pl.F == 0 && pl.R == nb && pl.pm && pl.items() > slots) {
       // several rounds of split blocks, piece-major: the items that start last are the blocks' last pieces, and the
       // launch ends with the slowest of them, so the last piece of every block takes tail_wb / 16 of the others'
@@ -3275,17 +3292,19 @@ int fwav_debug_topk_plan_cover(int64_t n, int rt, int pieces, int wide, int32_t*
 // The first pass fwav_sim_topk would launch for max_q queries over nd domains on the current device (no launch):
 // geometry (1 = wide), first-pass mode (0 = S16, 1 = HL), whole-table blocks F, split blocks R, pieces P (−1: query
 // halves), grid.
-// The default first-pass plan's chunk range of every table piece (piece_chunks, with the floor as the launch would
-// decide it): c01[2p], c01[2p + 1] = [c0, c1) of piece p < *np (at most kMaxPieces); *np = 1 for an unsplit plan.
-int fwav_debug_topk_piece_chunks(int64_t max_q, int64_t nd, int32_t* c01, int32_t* np) {
-  FWAV_CHECK_ARG(max_q > 0 && nd > 0 && c01 && np, FWAV_ERR_ARG, "fwav_debug_topk_piece_chunks: bad args");
+// The default first-pass plan's chunk range of every table piece of split block `block` (mod the split blocks;
+// piece_chunks, with the floor as the launch would decide it): c01[2p], c01[2p + 1] = [c0, c1) of piece p < *np (at
+// most kMaxPieces); *np = 1 for an unsplit plan.
+int fwav_debug_topk_piece_chunks(int64_t max_q, int64_t nd, int64_t block, int32_t* c01, int32_t* np) {
+  FWAV_CHECK_ARG(max_q > 0 && nd > 0 && block >= 0 && c01 && np, FWAV_ERR_ARG, "fwav_debug_topk_piece_chunks: bad args");
   const int geo = first_geometry(nd, max_q);
   int rt, P;
   host_plan_for(max_q, nd, geo, rt, P);
   const TopkPlan pl = make_plan(max_q, rt, P, geometry_qb(geo));
   const int n = pl.halves || pl.R == 0 ? 1 : pl.P;
   const int nchunks = (int)cdiv(nd, kChunk);
-  for (int p = 0; p < n; ++p) piece_chunks(pl, p, n, nchunks, c01[2 * p], c01[2 * p + 1]);
+  const int64_t b = pl.F + (pl.R > 0 ? block % pl.R : 0);  // a split block
+  for (int p = 0; p < n; ++p) piece_chunks(pl, b, p, n, nchunks, c01[2 * p], c01[2 * p + 1]);
   *np = n;
   return FWAV_OK;
 }

@@ -76,7 +76,7 @@ DEBUG_SIGNATURES = {
     "fwav_debug_topk_mode": (I32, [I32]),
     "fwav_debug_topk_geometry": (I32, [I32]),
     "fwav_debug_topk_plan_info": (I32, [I64, I64, P, P]),
-    "fwav_debug_topk_piece_chunks": (I32, [I64, I64, P, P]),
+    "fwav_debug_topk_piece_chunks": (I32, [I64, I64, I64, P, P]),
     "fwav_debug_topk_qb": (I64, [I32]),
     "fwav_debug_topk_floor": (I32, [I32, F32]),
     "fwav_debug_topk_floor_pieces": (I32, [I32]),

@@ -35,10 +35,11 @@ int fwav_debug_topk_tail(int wb);
  * pieces per split block (−1: query halves); blocks[0] = whole-table blocks, blocks[1] = split blocks,
  * blocks[2] = grid. */
 int fwav_debug_topk_plan_info(int64_t max_q, int64_t n_domains, int32_t* info, int64_t* blocks);
-/* The default plan's table pieces for max_q queries over n_domains (host only): c01[2p .. 2p + 1] = the chunk range
- * [c0, c1) of piece p (256-domain chunks) for p < *np (≤ 64; 1 when the plan splits no block).  One-round and
- * multi-round plans weigh some pieces unevenly; the ranges always tile the table. */
-int fwav_debug_topk_piece_chunks(int64_t max_q, int64_t n_domains, int32_t* c01, int32_t* np);
+/* The default plan's table pieces for max_q queries over n_domains (host only), of split block `block` (taken modulo
+ * the split blocks): c01[2p .. 2p + 1] = the chunk range [c0, c1) of piece p (256-domain chunks) for p < *np (≤ 64;
+ * 1 when the plan splits no block).  One-round and multi-round plans weigh some pieces unevenly; the
+ * ranges always tile the table. */
+int fwav_debug_topk_piece_chunks(int64_t max_q, int64_t n_domains, int64_t block, int32_t* c01, int32_t* np);
 /* Host-side check of a work plan (no device): count[position] += 1 for every query slot of every item of the plan of
  * n queries (whole blocks and query halves cover a query once, a block in P table pieces P times) in first-pass
  * geometry `wide` (0 = base, 1 = wide, 2 = centroid, 3 = centroid wide); *items = grid. */

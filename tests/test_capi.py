@@ -234,22 +234,28 @@ def test_work_plan_covers_every_query(lib, n, rt, pieces, wide):
                                    (2700000, 86398977)])
 def test_default_plan_pieces_tile_the_table(lib, nq, nd):
     """Host-side: the default plan's table pieces (piece_chunks, uneven where a one-round plan pairs older and younger
-    workgroups or a multi-round plan lightens its last piece) tile [0, ⌈nd/256⌉) without gaps or empty pieces; at one
-    rank's eighth of cfg2 the younger pieces are the smaller ones, at cfg2 the last piece is."""
-    c01 = np.zeros(2 * 64, np.int32)
-    n = ctypes.c_int32()
-    with lib.debug_library():
-        lib.call("fwav_debug_topk_piece_chunks", nq, nd, c01.ctypes.data, ctypes.addressof(n))
-    P = n.value
+    workgroups or a multi-round plan lightens its last piece) tile [0, ⌈nd/256⌉) without gaps or empty pieces, for
+    every split block; in one rank's eighth of cfg2 a block's pieces whose items start past slot 256 (the CUs' younger
+    workgroups) are the smaller ones, at cfg2 and at a quarter of it (several rounds) the last piece is."""
     nchunks = -(-nd // 256)
-    c0, c1 = c01[0:2 * P:2], c01[1:2 * P:2]
-    assert 1 <= P <= 64 and c0[0] == 0 and c1[-1] == nchunks
-    assert np.array_equal(c0[1:], c1[:-1]) and np.all(c1 > c0)
-    size = c1 - c0
-    if (nq, nd) == (41344, 1321977):  # 81 centroid blocks × 6 pieces: one round, pieces 3–5 younger
-        assert P == 6 and size[:3].min() > size[3:].max()
-    if (nq, nd) == (330750, 1321977):  # 646 blocks × 3 pieces over ≈ 3.8 rounds: the last piece lighter
-        assert P == 3 and size[2] < size[0] and abs(int(size[0]) - int(size[1])) <= 1
+    for block in (0, 1, 93, 94, 160, 161, 200, 645):
+        c01 = np.zeros(2 * 64, np.int32)
+        n = ctypes.c_int32()
+        with lib.debug_library():
+            lib.call("fwav_debug_topk_piece_chunks", nq, nd, block, c01.ctypes.data, ctypes.addressof(n))
+        P = n.value
+        c0, c1 = c01[0:2 * P:2], c01[1:2 * P:2]
+        assert 1 <= P <= 64 and c0[0] == 0 and c1[-1] == nchunks
+        assert np.array_equal(c0[1:], c1[:-1]) and np.all(c1 > c0)
+        size = c1 - c0
+        if (nq, nd) == (41344, 1321977):  # one round of 81 blocks × 6 pieces; slots 256 + 256
+            b = block % 81
+            older = np.array([p * 81 + b < 256 for p in range(P)])
+            assert P == 6 and older.any() and (~older).any()
+            assert size[older].min() > size[~older].max(), (block, size, older)
+        if (nq, nd) in ((330750, 1321977), (82688, 1321977)):  # several rounds (646 × 3, 162 × 6): the last piece lighter
+            assert P == {330750: 3, 82688: 6}[nq] and size[-1] < size[:-1].min()
+            assert size[:-1].max() - size[:-1].min() <= 1
 
 
 _MAPS = r"""
