@@ -2604,9 +2604,14 @@ static void floor_plan(int64_t max_q, int64_t nd, int& rt, int& P) {
   topk_device_slots(kGeoBase, cus, per_cu);
   const int64_t blocks = cdiv(cdiv(max_q > 0 ? max_q : 1, 50), k16QB);  // ≈ 2 % of the launch, in 256-query blocks
   const int64_t slots = (int64_t)cus * per_cu;
+  // 64 pieces where they fit one round, else as many from 16 to 32 as fit it (cfg2, ≈ 4,200–5,600 misses, 21–26
+  // blocks expected: 19 pieces 13.82 vs 13.87–13.92 ms with 16, and 23 / 26 / 30 faster still on the misses of that
+  // run, 17 blocks — but the floor's miss count varies run to run, so the round is sized for the 2 % estimate;
+  // profiles/r06/floor_p2_sweep.log)
+  const int64_t per = blocks > 0 ? slots / blocks : kFloorP2Fewest;
   const int p2 = g_floor_p2 > 0 ? g_floor_p2
-                                : (blocks * kFloorP2Fewest <= slots ? kFloorP2Fewest
-                                                                    : (blocks * kFloorP2Few <= slots ? kFloorP2Few : kFloorP2));
+                                : (per >= kFloorP2Fewest ? kFloorP2Fewest
+                                                         : (int)std::max<int64_t>(kFloorP2, std::min<int64_t>(per, kFloorP2Few)));
   P = (int)std::max<int64_t>(1, std::min<int64_t>(p2, pmax));
 }
 

@@ -67,7 +67,7 @@ int64_t fwav_debug_topk_qb(int geo);
  * All return the same candidates. */
 int fwav_debug_topk_floor(int mode, float value);
 /* Diagnostic override of the floor's second pass: table pieces per split block of misses (1 … 64; 0 = the default:
- * the most of 64 / 32 / 16 with which the expected misses fill one round of workgroups).  Re-query
+ * 64 where the expected misses fill one round of workgroups with them, else as many from 16 to 32 as do).  Re-query
  * fwav_sim_topk_workspace_size afterwards.  All return the same candidates. */
 int fwav_debug_topk_floor_pieces(int pieces);
 /* Byte offsets of the fp16 search's workspace regions (K <= 64) for max_q queries over n_domains domains, as this
