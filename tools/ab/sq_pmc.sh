@@ -2,7 +2,6 @@
 # SQ issue counters of the search kernel (cfg2, product geometry): two PMC passes of tools/topk_once.py
 set -euo pipefail
 export TMPDIR=/tmp
-rm -rf gpurun_out/sq/p1 gpurun_out/sq/p2 gpurun_out/sq/p3  # (tools/sq_summary.py reads one CSV per pass directory)
 mkdir -p gpurun_out/sq
 timeout -s KILL 120 rocprofv3 -L > gpurun_out/sq/list.txt 2>&1 || true
 pass() {  # name counters...

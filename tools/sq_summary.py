@@ -21,7 +21,8 @@ def load(root):
         if not fs:
             continue
         per = collections.defaultdict(lambda: collections.defaultdict(float))
-        for r in csv.DictReader(open(fs[0])):
+        # the newest pass file (gpurun merges each call's files into the same directory)
+        for r in csv.DictReader(open(max(fs, key=os.path.getmtime))):
             if "sim_topk" in r["Kernel_Name"]:
                 per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
         if per:  # the last big dispatch (the timed repetition)
